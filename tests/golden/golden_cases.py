@@ -1,0 +1,77 @@
+"""Case definitions shared by the golden generator and the parity tests.
+
+Pure data: no reference import.  Weights for every case are re-created with
+oracle.fill.named_fill_(seed), inputs with oracle.fill.randn(seed+k, shape).
+"""
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+# copied config.json values we need live in w2v_config.json next to this file
+W2V_CONFIG_JSON = os.path.join(HERE, "w2v_config.json")
+
+# WindowAttention3D (video_swin_transformer.py:91-173)
+WATTN_CASES = [
+    # shifted window, N=196, with compute_mask over a 4x14x14 volume (nW = 4)
+    dict(name="wattn_n196_mask", dim=64, heads=2, full_window=(4, 7, 7), N=196, B_=4,
+         mask_dhw=(4, 14, 14), shift=(2, 3, 3), seed=11),
+    # N=392 (Swin-T 8x7x7), unshifted, 3 heads of 32
+    dict(name="wattn_n392", dim=96, heads=3, full_window=(8, 7, 7), N=392, B_=2, seed=21),
+    # Q3: clamped window 4x4x4 (N=64) indexing the full 4x7x7 RPB table
+    dict(name="wattn_n64_clamped", dim=64, heads=2, full_window=(4, 7, 7), N=64, B_=2, seed=31),
+]
+
+# SwinTransformerBlock3D (:176-278)
+BLOCK_CASES = [
+    dict(name="block_shift", dim=64, heads=2, window=(4, 7, 7), shift=(2, 3, 3), shape=(1, 4, 14, 14), seed=41),
+    dict(name="block_noshift", dim=64, heads=2, window=(4, 7, 7), shift=(0, 0, 0), shape=(1, 4, 14, 14), seed=51),
+    # padded H/W (10 -> 14), shifted: exercises pad-after-LN and the mask over padded volume
+    dict(name="block_pad_shift", dim=64, heads=2, window=(4, 7, 7), shift=(2, 3, 3), shape=(1, 4, 10, 10), seed=61),
+    # clamped D (2 <= 4 -> window 2, shift 0 along D), shift only along H/W
+    dict(name="block_clampD", dim=64, heads=2, window=(4, 7, 7), shift=(2, 3, 3), shape=(2, 2, 14, 14), seed=71),
+]
+
+PATCH_EMBED = dict(name="patch_embed", patch=(2, 4, 4), dim=96, shape=(2, 3, 8, 32, 32), seed=81)
+MERGE_CASES = [
+    dict(name="merge_even", dim=64, shape=(1, 4, 14, 14, 64), seed=91),
+    dict(name="merge_odd", dim=64, shape=(1, 2, 7, 7, 64), seed=101),
+]
+
+VST_C1 = dict(name="vst_c1", seed=111, shape=(1, 3, 8, 112, 112),
+              kwargs=dict(patch_size=(2, 4, 4), embed_dim=96, depths=[2, 2, 2, 2], num_heads=[3, 6, 12, 24],
+                          window_size=(4, 7, 7), drop_path_rate=0.0, patch_norm=True))
+
+
+def w2v_overrides(layers):
+    """Deterministic wav2vec2 (Q12): every dropout, LayerDrop and SpecAugment off."""
+    return dict(num_hidden_layers=layers, hidden_dropout=0.0, attention_dropout=0.0, activation_dropout=0.0,
+                feat_proj_dropout=0.0, layerdrop=0.0, mask_time_prob=0.0, final_dropout=0.0,
+                hidden_dropout_prob=0.0)
+
+
+W2V_C1 = dict(name="w2v_2layer_1s", layers=2, B=1, seconds=1, seed=121)
+W2V_GRAD_KEYS = ("conv_layers.0.conv.weight", "conv_layers.0.layer_norm", "conv_layers.3.conv.weight",
+                 "feature_projection", "pos_conv_embed", "layers.0.attention.q_proj", "layers.1.feed_forward",
+                 "encoder.layer_norm", "layers.1.final_layer_norm")
+
+HEAD = dict(name="fusion_head", B=4, video_dim=768, audio_dim=256, seed=131)
+
+FUSED_C1 = dict(
+    name="fused_c1", seed=141, B=2, T=8, H=112, W=112, seconds=1, lr=0.01, wd=0.05,
+    vst=VST_C1["kwargs"],
+    mel=dict(num_classes=1, use_feat=True, img_size=224, embed_dim=32, depths=[2, 2, 2, 2], num_heads=[1, 2, 4, 8],
+             window_size=7, drop_path_rate=0.0, pretrained_window_sizes=(16, 16, 16, 16)),
+    w2v_layers=2, video_dim=768, audio_dim=256)
+
+
+def fixture_compress(key, a, big=65536):
+    """Tensors above ``big`` elements are stored as key@sub (every step-th
+    element of the flat array), key@sum and key@norm (float64)."""
+    import numpy as np
+    a = np.asarray(a)
+    if a.size <= big:
+        return {key: a}
+    step = -(-a.size // 8192)
+    f = a.reshape(-1).astype(np.float64)
+    return {key + "@sub": a.reshape(-1)[::step].copy(), key + "@step": np.array(step),
+            key + "@shape": np.array(a.shape), key + "@sum": np.array(f.sum()),
+            key + "@norm": np.array(np.sqrt((f * f).sum()))}

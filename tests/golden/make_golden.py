@@ -1,0 +1,221 @@
+"""Generate golden vectors by running the REFERENCE modules on CPU (fp32).
+
+Run in the build container only (needs /root/reference):
+    python tests/golden/make_golden.py
+Writes tests/golden/*.npz.  Weights are never stored: every case re-creates
+them with oracle.fill.named_fill_ (deterministic per state_dict key), and
+inputs / upstream gradients come from oracle.fill.randn / synthetic_inputs
+(seeded Philox streams), so the fixtures hold inputs only when tiny and always
+the reference outputs.
+
+Cases follow SURVEY.md §8c "Golden vectors to commit".
+"""
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+from refimport import import_reference  # noqa: E402
+from oracle.fill import named_fill_, randn, synthetic_inputs  # noqa: E402
+import golden_cases as GC  # noqa: E402
+
+R = import_reference()
+torch = R.torch
+torch.set_num_threads(8)
+VST = R.VST
+
+
+BIG = 65536  # larger tensors are stored as a strided sample + sum + norm (fixture_compress)
+
+
+def save(name, **arrays):
+    out = {}
+    for k, v in arrays.items():
+        a = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
+        out.update(GC.fixture_compress(k, a, BIG))
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: " + ", ".join(f"{k}{tuple(v.shape)}" for k, v in out.items()))
+
+
+def grads_of(module, prefix=""):
+    return {("g:" + prefix + n): p.grad.clone() for n, p in module.named_parameters() if p.grad is not None}
+
+
+# ---------------------------------------------------------------- VST pieces
+def case_window_attention():
+    for c in GC.WATTN_CASES:
+        m = VST.WindowAttention3D(c["dim"], c["full_window"], c["heads"], qkv_bias=True)
+        named_fill_(m, seed=c["seed"])
+        x = randn(c["seed"] + 1, (c["B_"], c["N"], c["dim"])).requires_grad_(True)
+        mask = None
+        if c.get("mask_dhw"):
+            D, H, W = c["mask_dhw"]
+            mask = VST.compute_mask(D, H, W, tuple(c["full_window"]), tuple(c["shift"]), torch.device("cpu"))
+        y = m(x, mask)
+        gy = randn(c["seed"] + 2, y.shape)
+        y.backward(gy)
+        save(c["name"], y=y, dx=x.grad, **grads_of(m))
+
+
+def case_block():
+    for c in GC.BLOCK_CASES:
+        m = VST.SwinTransformerBlock3D(c["dim"], c["heads"], window_size=tuple(c["window"]),
+                                       shift_size=tuple(c["shift"]), qkv_bias=True)
+        named_fill_(m, seed=c["seed"])
+        B, D, H, W = c["shape"]
+        x = randn(c["seed"] + 1, (B, D, H, W, c["dim"])).requires_grad_(True)
+        ws, ss = VST.get_window_size((D, H, W), tuple(c["window"]), tuple(c["shift"]))
+        Dp = -(-D // ws[0]) * ws[0]
+        Hp = -(-H // ws[1]) * ws[1]
+        Wp = -(-W // ws[2]) * ws[2]
+        mask = VST.compute_mask(Dp, Hp, Wp, ws, ss, torch.device("cpu"))
+        y = m(x, mask)
+        gy = randn(c["seed"] + 2, y.shape)
+        y.backward(gy)
+        save(c["name"], y=y, dx=x.grad, **grads_of(m))
+
+
+def case_patch_embed_merge():
+    c = GC.PATCH_EMBED
+    m = VST.PatchEmbed3D(tuple(c["patch"]), 3, c["dim"], norm_layer=torch.nn.LayerNorm)
+    named_fill_(m, seed=c["seed"])
+    x = randn(c["seed"] + 1, c["shape"])
+    y = m(x)
+    gy = randn(c["seed"] + 2, y.shape)
+    y.backward(gy)
+    save(c["name"], y=y, **grads_of(m))
+    for c in GC.MERGE_CASES:
+        m = VST.PatchMerging(c["dim"])
+        named_fill_(m, seed=c["seed"])
+        x = randn(c["seed"] + 1, c["shape"]).requires_grad_(True)
+        y = m(x)
+        gy = randn(c["seed"] + 2, y.shape)
+        y.backward(gy)
+        save(c["name"], y=y, dx=x.grad, **grads_of(m))
+
+
+def case_vst_c1():
+    c = GC.VST_C1
+    m = VST.SwinTransformer3D(**c["kwargs"])
+    named_fill_(m, seed=c["seed"])
+    m.eval()  # (Q2: returns None, do not chain)
+    x = randn(c["seed"] + 1, c["shape"])
+    with torch.no_grad():
+        y = m(x)
+    save(c["name"], y=y)
+
+
+# ------------------------------------------------------------------ wav2vec2
+def w2v_model(layers):
+    from transformers import Wav2Vec2Config, Wav2Vec2Model
+    cfg = Wav2Vec2Config.from_json_file(GC.W2V_CONFIG_JSON)
+    for k, v in GC.w2v_overrides(layers).items():
+        setattr(cfg, k, v)
+    cfg._attn_implementation = "eager"
+    return Wav2Vec2Model(cfg)
+
+
+def case_w2v():
+    c = GC.W2V_C1
+    m = w2v_model(c["layers"])
+    named_fill_(m, seed=c["seed"])
+    m.train()  # all stochastic pieces are disabled by w2v_overrides
+    _, _, wave, _ = synthetic_inputs(c["B"], 2, 16, 16, c["seconds"], seed=c["seed"] + 1)
+    out = m(wave)
+    h = out.last_hidden_state
+    gy = randn(c["seed"] + 2, h.shape)
+    h.backward(gy)
+    g = grads_of(m)
+    keep = {k: v for k, v in g.items() if any(s in k for s in GC.W2V_GRAD_KEYS)}
+    save(c["name"], y=h, extract=out.extract_features, **keep)
+
+
+# -------------------------------------------------------------- fusion head
+class _Ident(torch.nn.Module):
+    def forward(self, x):
+        return x
+
+
+def case_head():
+    c = GC.HEAD
+    args = types.SimpleNamespace(soft=0.01, classify_drop=0.0, swin_drop=0.0)
+    m = R.FusionModel(args, _Ident(), _Ident(), _Ident(), out_dim=1, video_dim=c["video_dim"],
+                      audio_dim=c["audio_dim"], paudio_dim=768)
+    named_fill_(m, seed=c["seed"])
+    B = c["B"]
+    fv = randn(c["seed"] + 1, (B, c["video_dim"])).requires_grad_(True)
+    fa = randn(c["seed"] + 2, (B, c["audio_dim"])).requires_grad_(True)
+    fp = randn(c["seed"] + 3, (B, 768)).requires_grad_(True)
+    logits = {}
+    m.classify.register_forward_hook(lambda mod, i, o: logits.__setitem__("z", o.detach().clone()))
+    m.train()
+    p = m((fv, fa, fp))
+    gy = randn(c["seed"] + 4, p.shape)
+    p.backward(gy)
+    out = dict(p_train=p, z_train=logits["z"], dfv=fv.grad, dfa=fa.grad, dfp=fp.grad,
+               rm=m.norm.running_mean, rv=m.norm.running_var, **grads_of(m))
+    m.eval()
+    with torch.no_grad():
+        pe = m((fv, fa, fp))
+    save(c["name"], p_eval=pe, z_eval=logits["z"], **out)
+
+
+# ----------------------------------------------------------- fused C1 model
+class VSTFeat(torch.nn.Module):
+    """Build glue (Q8): [B,T,C,H,W] -> permute -> SwinTransformer3D -> mean(D,H,W)."""
+    def __init__(self, vst):
+        super().__init__()
+        self.vst = vst
+
+    def forward(self, x):
+        return self.vst(x.permute(0, 2, 1, 3, 4)).mean(dim=[2, 3, 4])
+
+
+def build_fused_ref(cfg):
+    args = types.SimpleNamespace(soft=0.01, classify_drop=0.0, swin_drop=0.0)
+    vst = VST.SwinTransformer3D(**cfg["vst"])
+    mel = R.SwinTransformerV2(**cfg["mel"])
+    w2v = w2v_model(cfg["w2v_layers"])
+    pa = R.Audio2D(args, w2v, num_classes=1, use_feat=True)
+    m = R.FusionModel(args, VSTFeat(vst), mel, pa, out_dim=1, video_dim=cfg["video_dim"],
+                      audio_dim=cfg["audio_dim"], paudio_dim=768)
+    return m
+
+
+def case_fused_c1():
+    c = GC.FUSED_C1
+    m = build_fused_ref(c)
+    named_fill_(m, seed=c["seed"])
+    video, mel, wave, label = synthetic_inputs(c["B"], c["T"], c["H"], c["W"], c["seconds"], seed=c["seed"] + 1)
+    logits = {}
+    m.classify.register_forward_hook(lambda mod, i, o: logits.__setitem__("z", o.detach().clone()))
+    m.eval()
+    with torch.no_grad():
+        pe = m((video, mel, wave))
+    z_eval = logits["z"]
+    # one training step exactly as src/trainer.py:80-88,124-148,280-297 (accum_step=1)
+    m.train()
+    opt = torch.optim.SGD(m.parameters(), lr=c["lr"], momentum=0.9, weight_decay=c["wd"])
+    opt.zero_grad()
+    p = m((video, mel, wave))
+    loss = torch.nn.BCELoss()(p, label)
+    loss.backward()
+    gnorm = {("gn:" + n): q.grad.norm() for n, q in m.named_parameters() if q.grad is not None}
+    opt.step()
+    psum = {("ps:" + n): q.detach().double().sum() for n, q in m.named_parameters()}
+    save(c["name"], p_eval=pe, z_eval=z_eval, p_train=p, z_train=logits["z"], loss=loss, **gnorm, **psum)
+
+
+if __name__ == "__main__":
+    only = sys.argv[1:]
+    for fn in [case_window_attention, case_block, case_patch_embed_merge, case_vst_c1, case_w2v, case_head,
+               case_fused_c1]:
+        if not only or fn.__name__ in only:
+            fn()
