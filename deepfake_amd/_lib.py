@@ -1,0 +1,105 @@
+"""ctypes binding of libdfk.so (the C ABI declared in include/dfk.h).
+
+The product path has no CPU fallback: importing this module without the
+built library, or calling an op with tensors that are not on a HIP device,
+raises.  Build with ``python -m deepfake_amd.build``.
+"""
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdfk.so")
+
+F32, BF16 = 0, 1
+
+
+class View(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("ld", C.c_int64), ("bs0", C.c_int64), ("bs1", C.c_int64),
+                ("conv_cg", C.c_int32), ("conv_stride", C.c_int32), ("conv_pad", C.c_int32),
+                ("conv_rows", C.c_int32)]
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [("a", View), ("b", View), ("c", C.c_void_p), ("bias", C.c_void_p), ("residual", C.c_void_p),
+                ("aux", C.c_void_p), ("ldc", C.c_int64), ("cbs0", C.c_int64), ("cbs1", C.c_int64),
+                ("ldr", C.c_int64), ("rbs0", C.c_int64), ("rbs1", C.c_int64), ("ldaux", C.c_int64),
+                ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("dtype", C.c_int32),
+                ("a_kmajor", C.c_int32), ("b_kmajor", C.c_int32), ("c_f32", C.c_int32), ("nz0", C.c_int32),
+                ("nz1", C.c_int32), ("splitk", C.c_int32), ("act", C.c_int32), ("atomic", C.c_int32),
+                ("beta", C.c_float)]
+
+
+class WattnArgs(C.Structure):
+    _fields_ = [("q", C.c_void_p), ("k", C.c_void_p), ("v", C.c_void_p), ("out", C.c_void_p),
+                ("rpb", C.c_void_p), ("pad_q", C.c_void_p), ("pad_k", C.c_void_p), ("pad_v", C.c_void_p),
+                ("lse", C.c_void_p), ("ld_qkv", C.c_int64), ("ld_out", C.c_int64),
+                ("B", C.c_int32), ("D", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
+                ("wd", C.c_int32), ("wh", C.c_int32), ("ww", C.c_int32),
+                ("fd", C.c_int32), ("fh", C.c_int32), ("fw", C.c_int32),
+                ("sd", C.c_int32), ("sh", C.c_int32), ("sw", C.c_int32),
+                ("heads", C.c_int32), ("hd", C.c_int32), ("dtype", C.c_int32), ("scale", C.c_float)]
+
+
+class WattnBwdArgs(C.Structure):
+    _fields_ = [("f", WattnArgs), ("dout", C.c_void_p), ("dq", C.c_void_p), ("dk", C.c_void_p),
+                ("dv", C.c_void_p), ("drpb", C.c_void_p), ("ld_dqkv", C.c_int64), ("ld_dout", C.c_int64)]
+
+
+# (name, restype, argtypes) for every exported symbol of include/dfk.h
+_VP, _I64, _I32, _F = C.c_void_p, C.c_int64, C.c_int32, C.c_float
+SIGNATURES = {
+    "dfk_gemm": [C.POINTER(GemmArgs), _VP],
+    "dfk_colsum": [_VP, C.c_int, _I64, _I64, _I64, _VP, _VP],
+    "dfk_layernorm_fwd": [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, _F, C.c_int, _VP],
+    "dfk_layernorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, C.c_int, C.c_int, _VP],
+    "dfk_wattn_fwd": [C.POINTER(WattnArgs), _VP],
+    "dfk_wattn_bwd": [C.POINTER(WattnBwdArgs), _VP],
+}
+
+_lib = None
+
+
+def lib():
+    """Load libdfk.so once; raise (never fall back) if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"deepfake_amd: {LIB_PATH} not built — run `python -m deepfake_amd.build`")
+        L = C.CDLL(LIB_PATH)
+        for name, argt in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = C.c_int
+            fn.argtypes = argt
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"deepfake_amd: {what} failed (rc={rc}{' EINVAL' if rc == -1 else ''})")
+
+
+def ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("deepfake_amd: tensors must be on the HIP device (no CPU fallback)")
+    return C.c_void_p(t.data_ptr())
+
+
+def dt(t):
+    if t.dtype == torch.bfloat16:
+        return BF16
+    if t.dtype == torch.float32:
+        return F32
+    raise TypeError(f"deepfake_amd: unsupported dtype {t.dtype}")

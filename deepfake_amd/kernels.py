@@ -1,0 +1,157 @@
+"""Thin tensor-level wrappers over the C ABI (include/dfk.h).
+
+Every function enqueues on torch's current HIP stream, allocates outputs with
+the torch caching allocator (graph-capture safe) and raises on any error.
+Activations are 2-D token-major views ([rows, C], contiguous rows).
+"""
+import math
+
+import torch
+
+from . import _lib as L
+
+_CU_TARGET_BLOCKS = 2048  # split-K target grid for skinny weight-gradient GEMMs
+
+
+def _view(t, ld, bs0=0, bs1=0, conv=None):
+    v = L.View()
+    v.ptr = t.data_ptr()
+    v.ld, v.bs0, v.bs1 = int(ld), int(bs0), int(bs1)
+    if conv:
+        v.conv_cg, v.conv_stride, v.conv_pad, v.conv_rows = (int(c) for c in conv)
+    return v
+
+
+def gemm(a, a_ld, a_kmajor, b, b_ld, b_kmajor, M, N, K, c, ldc, *, dtype, c_f32=False, bias=None,
+         residual=None, ldr=0, aux=None, ldaux=0, act=0, beta=0.0, atomic=False, splitk=1,
+         nz=(1, 1), a_bs=(0, 0), b_bs=(0, 0), c_bs=(0, 0), r_bs=(0, 0), a_conv=None, b_conv=None):
+    """Raw dfk_gemm.  a/b/c are tensors (base pointers); see include/dfk.h."""
+    g = L.GemmArgs()
+    g.a = _view(a, a_ld, *a_bs, conv=a_conv)
+    g.b = _view(b, b_ld, *b_bs, conv=b_conv)
+    g.c = c.data_ptr()
+    g.bias = bias.data_ptr() if bias is not None else None
+    g.residual = residual.data_ptr() if residual is not None else None
+    g.aux = aux.data_ptr() if aux is not None else None
+    g.ldc, g.cbs0, g.cbs1 = int(ldc), int(c_bs[0]), int(c_bs[1])
+    g.ldr, g.rbs0, g.rbs1 = int(ldr), int(r_bs[0]), int(r_bs[1])
+    g.ldaux = int(ldaux)
+    g.M, g.N, g.K = int(M), int(N), int(K)
+    g.dtype = dtype
+    g.a_kmajor, g.b_kmajor = int(a_kmajor), int(b_kmajor)
+    g.c_f32 = int(c_f32)
+    g.nz0, g.nz1 = int(nz[0]), int(nz[1])
+    g.splitk = int(splitk)
+    g.act = int(act)
+    g.atomic = int(atomic)
+    g.beta = float(beta)
+    for t in (a, b, c):
+        if not t.is_cuda:
+            raise RuntimeError("deepfake_amd: tensors must be on the HIP device (no CPU fallback)")
+    L.check(L.lib().dfk_gemm(g, L.stream()), f"gemm M={M} N={N} K={K}")
+
+
+def linear(x, w, b=None, act=0, aux=None, residual=None, out=None, beta=0.0):
+    """y[M,N] = x[M,K] @ w[N,K]^T (+b) (gelu: act=1, preact -> aux) (+residual)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    gemm(x, x.stride(0), False, w, w.stride(0), False, M, N, K, out, out.stride(0), dtype=L.dt(x), bias=b,
+         residual=residual, ldr=residual.stride(0) if residual is not None else 0, aux=aux,
+         ldaux=aux.stride(0) if aux is not None else 0, act=act, beta=beta)
+    return out
+
+
+def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0):
+    """dx[M,K] = dy[M,N] @ w[N,K]  (act=2: times gelu'(aux))."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if out is None:
+        out = torch.empty(M, K, device=dy.device, dtype=dy.dtype)
+    gemm(dy, dy.stride(0), False, w, w.stride(0), True, M, K, N, out, out.stride(0), dtype=L.dt(dy), act=act,
+         aux=aux, ldaux=aux.stride(0) if aux is not None else 0, beta=beta)
+    return out
+
+
+def splitk_for(tiles, K, min_k=256):
+    return max(1, min(_CU_TARGET_BLOCKS // max(tiles, 1), max(K // min_k, 1)))
+
+
+def linear_dw(dy, x, dw):
+    """dw[N,K] (fp32, +=) += dy[M,N]^T @ x[M,K]  (split over M, fp32 atomics)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    tiles = math.ceil(N / 128) * math.ceil(K / 128)
+    gemm(dy, dy.stride(0), True, x, x.stride(0), True, N, K, M, dw, dw.stride(0), dtype=L.dt(dy), c_f32=True,
+         atomic=True, splitk=splitk_for(tiles, M))
+    return dw
+
+
+def colsum(x, out):
+    """out[j] (fp32) += sum_i x[i, j]."""
+    rows, cols = x.shape
+    L.check(L.lib().dfk_colsum(L.ptr(x), L.dt(x), rows, cols, x.stride(0), L.ptr(out), L.stream()), "colsum")
+    return out
+
+
+def layernorm_fwd(x, w, b, eps=1e-5, out=None):
+    rows, C = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    L.check(L.lib().dfk_layernorm_fwd(L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(out), L.ptr(mean), L.ptr(rstd), rows, C,
+                                      float(eps), L.dt(x), L.stream()), "layernorm_fwd")
+    return out, mean, rstd
+
+
+def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False):
+    rows, C = x.shape
+    if dx is None:
+        dx = torch.empty_like(x)
+    L.check(L.lib().dfk_layernorm_bwd(L.ptr(dy), L.ptr(x), L.ptr(w), L.ptr(mean), L.ptr(rstd), L.ptr(dx),
+                                      L.ptr(dw), L.ptr(db), rows, C, int(accumulate), L.dt(x), L.stream()),
+            "layernorm_bwd")
+    return dx
+
+
+def wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb=None, pads=None,
+               lse=None):
+    a = L.WattnArgs()
+    a.q, a.k, a.v, a.out = q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
+    a.rpb = rpb.data_ptr() if rpb is not None else None
+    if pads is not None:
+        a.pad_q, a.pad_k, a.pad_v = (p.data_ptr() for p in pads)
+    a.lse = lse.data_ptr() if lse is not None else None
+    a.ld_qkv, a.ld_out = int(ld_qkv), int(out.stride(-2) if out.dim() > 1 else heads * hd)
+    a.B, a.D, a.H, a.W = (int(d) for d in dims)
+    a.wd, a.wh, a.ww = (int(w) for w in window)
+    a.fd, a.fh, a.fw = (int(w) for w in full_window)
+    a.sd, a.sh, a.sw = (int(s) for s in shift)
+    a.heads, a.hd = int(heads), int(hd)
+    a.dtype = L.dt(q)
+    a.scale = float(scale)
+    return a
+
+
+def window_geometry(dims, window):
+    B, D, H, W = dims
+    Dp, Hp, Wp = (math.ceil(n / w) * w for n, w in zip((D, H, W), window))
+    nW = (Dp // window[0]) * (Hp // window[1]) * (Wp // window[2])
+    N = window[0] * window[1] * window[2]
+    Np = math.ceil(N / 32) * 32
+    return nW, N, Np
+
+
+def wattn_fwd(q, k, v, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb=None, pads=None,
+              out=None, need_lse=True):
+    """Token-major window attention core; returns (out [rows, heads*hd], lse)."""
+    rows = dims[0] * dims[1] * dims[2] * dims[3]
+    if out is None:
+        out = torch.empty(rows, heads * hd, device=q.device, dtype=q.dtype)
+    nW, N, Np = window_geometry(dims, window)
+    lse = torch.empty(dims[0] * nW * heads, Np, device=q.device, dtype=torch.float32) if need_lse else None
+    a = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse)
+    L.check(L.lib().dfk_wattn_fwd(a, L.stream()), "wattn_fwd")
+    return out, lse

@@ -1,0 +1,133 @@
+/*
+ * dfk.h — C ABI of the DeepFake MI355X (gfx950) hot-path library libdfk.so.
+ *
+ * The reference (Polarisjame/DeepFake @ 2024_10_08) has no FFI: its hot path
+ * is plain nn.Module code on stock PyTorch ops.  These entry points are the
+ * native layer below the same nn.Module surface; each cites
+ * the reference op(s) it replaces.  Conventions for every entry point:
+ *   - plain device pointers + sizes; the caller owns every buffer (no
+ *     allocation inside, no host synchronisation: graph-capturable);
+ *   - work is enqueued on the given hipStream_t;
+ *   - returns 0 on success, a hipError_t value on a launch error, or
+ *     DFK_EINVAL (-1) when arguments violate the documented contract;
+ *   - dtype: DFK_F32 (0) or DFK_BF16 (1) for activations / weights; all
+ *     reductions and statistics are fp32.
+ */
+#ifndef DFK_H
+#define DFK_H
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DFK_F32 0
+#define DFK_BF16 1
+#define DFK_EINVAL (-1)
+
+/* A 2-D operand view V(r, c), contiguous along c.
+ *  plain: V(r,c) = ptr[r*ld + c]
+ *  conv : V(r,c) = ptr[(r*conv_stride + c/conv_cg - conv_pad)*ld + c%conv_cg]   (0 outside [0,conv_rows))
+ *         an implicit-GEMM view of a channels-last 1-D convolution input.
+ * Batched launches index z = z0*nz1 + z1 and add z0*bs0 + z1*bs1 elements. */
+typedef struct {
+  const void* ptr;
+  int64_t ld;
+  int64_t bs0;
+  int64_t bs1;
+  int32_t conv_cg;      /* 0 = plain view */
+  int32_t conv_stride;
+  int32_t conv_pad;
+  int32_t conv_rows;
+} dfk_view;
+
+/* C[i,j] (+)= sum_k A(i,k) B(k,j) with fused prologue/epilogue.
+ *  A(i,k) = a_kmajor ? a.V(k,i) : a.V(i,k);   B(k,j) = b_kmajor ? b.V(k,j) : b.V(j,k)
+ * Replaces every nn.Linear forward (y = x W^T + b) and its two backward GEMMs
+ * (dx = dy W, dW = dy^T x), and the wav2vec2 Conv1d stack as implicit GEMM:
+ *   video_swin_transformer.py:134,136 (qkv/proj), src/utils.py:249-251 (Mlp),
+ *   :291 (PatchMerging.reduction), ModalFusion.py:16-25, HF modeling_wav2vec2.py
+ *   :258-272 (conv1..6), :326-368 (pos-conv), :495-498,:556-561 (encoder linears).
+ * Epilogue, in order: +bias[j]; act==1: aux<-v (if aux), v=gelu(v);
+ *   act==2: v *= gelu'(aux[i,j]); +residual[i,j]; then store
+ *   (beta: v += beta*C_old) or fp32 atomicAdd (atomic=1, for split-K / batch-summed weight grads).
+ * Contract: the contiguous extent and ld of each view are multiples of 8 (bf16) / 4 (f32). */
+typedef struct {
+  dfk_view a;
+  dfk_view b;
+  void* c;
+  const void* bias;
+  const void* residual;
+  void* aux;
+  int64_t ldc, cbs0, cbs1;
+  int64_t ldr, rbs0, rbs1;
+  int64_t ldaux;
+  int32_t M, N, K;
+  int32_t dtype;        /* of A, B, bias, residual, aux (and C unless c_f32) */
+  int32_t a_kmajor, b_kmajor;
+  int32_t c_f32;
+  int32_t nz0, nz1;
+  int32_t splitk;
+  int32_t act;
+  int32_t atomic;
+  float beta;
+} dfk_gemm_args;
+int dfk_gemm(const dfk_gemm_args* g, hipStream_t stream);
+
+/* out[j] (+)= sum_i x[i*ld + j] (fp32 atomics).  Linear bias gradients. */
+int dfk_colsum(const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld, float* out, hipStream_t stream);
+
+/* LayerNorm over the last dim C of `rows` rows (nn.LayerNorm / F.layer_norm,
+ * video_swin_transformer.py:209,215,292,548,678; HF :424,:586-588,:661).
+ * y = (x-mean)*rstd*w + b; saves mean/rstd (fp32) for the backward. */
+int dfk_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
+                      int64_t rows, int32_t C, float eps, int dtype, hipStream_t stream);
+/* dx (=, or += when accumulate) ; dw, db accumulate (fp32 atomics). */
+int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                      void* dx, float* dw, float* db, int64_t rows, int32_t C, int accumulate, int dtype,
+                      hipStream_t stream);
+
+/* Windowed multi-head attention core on token-major buffers (no window
+ * partition / roll copies: both are index arithmetic inside the kernel).
+ * Replaces WindowAttention3D.forward (video_swin_transformer.py:148-170) with
+ * forward_part1's pad/roll/window_partition/window_reverse/roll/crop (:224-252),
+ * and eager_attention_forward of wav2vec2 (HF :438-463) as a single window.
+ *   q/k/v: element (b, d, h, w, head, e) at ptr[((b*D+d)*H+h)*W+w)*ld + head*hd + e]
+ *   out  : same indexing with ld_out.
+ *   window (wd,wh,ww) = clamped window; full_window = RPB decode geometry (Q3);
+ *   shift along each dim (0 = none); positions padded up to the window grid
+ *   read the qkv bias (`pad_q/k/v`, zero input after LN, :229) .
+ *   rpb: [L, nH] fp32 table or NULL;  mask: shifted-window 0/-100 mask (Q4)
+ *   applied iff any shift > 0.  scale multiplies q before q k^T (Q5).
+ *   lse (fp32 [B*nW, nH, Np]) saved for the backward. */
+typedef struct {
+  const void* q; const void* k; const void* v;
+  void* out;
+  const float* rpb;
+  const void* pad_q; const void* pad_k; const void* pad_v;
+  float* lse;
+  int64_t ld_qkv, ld_out;
+  int32_t B, D, H, W;
+  int32_t wd, wh, ww;
+  int32_t fd, fh, fw;
+  int32_t sd, sh, sw;
+  int32_t heads, hd;
+  int32_t dtype;
+  float scale;
+} dfk_wattn_args;
+int dfk_wattn_fwd(const dfk_wattn_args* a, hipStream_t stream);
+/* backward: dq/dk/dv written at the q/k/v layout (ld_dqkv); drpb [L,nH] fp32 (+=). */
+typedef struct {
+  dfk_wattn_args f;
+  const void* dout;
+  void* dq; void* dk; void* dv;
+  float* drpb;
+  int64_t ld_dqkv, ld_dout;
+} dfk_wattn_bwd_args;
+int dfk_wattn_bwd(const dfk_wattn_bwd_args* a, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

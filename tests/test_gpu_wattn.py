@@ -1,0 +1,68 @@
+"""GPU: window-attention core vs a torch fp32 reference (gather formulation of oracle/vst.py)."""
+import math
+
+import pytest
+import torch
+
+from oracle import vst as OV
+
+pytestmark = pytest.mark.gpu
+if torch.cuda.is_available():
+    from deepfake_amd import kernels as K
+
+DEV = "cuda"
+
+CASES = [
+    # dims(B,D,H,W), window(clamped), full window, shift, heads, hd
+    ((1, 4, 14, 14), (4, 7, 7), (4, 7, 7), (2, 3, 3), 2, 32),
+    ((2, 8, 14, 14), (8, 7, 7), (8, 7, 7), (0, 0, 0), 3, 32),
+    ((1, 4, 10, 10), (4, 7, 7), (4, 7, 7), (2, 3, 3), 2, 32),     # padded H/W
+    ((2, 4, 4, 4), (4, 4, 4), (4, 7, 7), (0, 0, 0), 4, 32),       # Q3 clamped window
+    ((3, 1, 1, 49), (1, 1, 49), (1, 1, 49), (0, 0, 0), 12, 64),   # wav2vec2 (T=49)
+    ((2, 1, 1, 199), (1, 1, 199), (1, 1, 199), (0, 0, 0), 4, 64), # wav2vec2 (T=199)
+]
+
+
+def ref_attention(qkv, pads, dims, window, full_window, shift, heads, hd, scale, rpb):
+    """fp32 torch: gather windows (pad with pad vectors, roll), softmax(q k^T s + rpb + mask) v, scatter."""
+    B, D, H, W = dims
+    C = heads * hd
+    Dp, Hp, Wp = (math.ceil(n / w) * w for n, w in zip((D, H, W), window))
+    x = torch.zeros(B, Dp, Hp, Wp, 3 * C, device=qkv.device)
+    x[...] = torch.cat(pads).float()
+    x[:, :D, :H, :W] = qkv.view(B, D, H, W, 3 * C).float()
+    tok = OV.window_token_index(Dp, Hp, Wp, window).to(qkv.device)
+    d, h, w = tok // (Hp * Wp), (tok // Wp) % Hp, tok % Wp
+    src = (((d + shift[0]) % Dp) * Hp + (h + shift[1]) % Hp) * Wp + (w + shift[2]) % Wp
+    nW, N = tok.shape
+    win = x.view(B, -1, 3 * C)[:, src.reshape(-1)].view(B * nW, N, 3, heads, hd)
+    q, k, v = (win[:, :, i].transpose(1, 2) for i in range(3))
+    s = (q * scale) @ k.transpose(-1, -2)
+    if rpb is not None:
+        idx = OV.rpb_index(full_window, N).to(qkv.device)
+        s = s + rpb[idx.reshape(-1)].view(N, N, heads).permute(2, 0, 1)[None]
+    if any(sh > 0 for sh in shift):
+        m = OV.shift_mask(Dp, Hp, Wp, window, shift).to(qkv.device)
+        s = (s.view(B, nW, heads, N, N) + m[None, :, None]).view(B * nW, heads, N, N)
+    o = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B, nW * N, C)
+    out = torch.zeros(B, Dp * Hp * Wp, C, device=qkv.device).index_copy(1, src.reshape(-1), o)
+    return out.view(B, Dp, Hp, Wp, C)[:, :D, :H, :W].reshape(-1, C)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
+def test_wattn_fwd(dt, case):
+    dims, window, fw, shift, heads, hd = case
+    g = torch.Generator(device=DEV).manual_seed(3)
+    rows = dims[0] * dims[1] * dims[2] * dims[3]
+    C = heads * hd
+    qkv = torch.randn(rows, 3 * C, device=DEV, generator=g).to(dt)
+    pads = [0.3 * torch.randn(C, device=DEV, generator=g).to(dt) for _ in range(3)]
+    L = (2 * fw[0] - 1) * (2 * fw[1] - 1) * (2 * fw[2] - 1)
+    rpb = torch.randn(L, heads, device=DEV, generator=g) * 0.5 if hd == 32 else None
+    scale = hd ** -0.5
+    out, lse = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, window, fw, shift, heads, hd, scale,
+                           rpb=rpb, pads=pads)
+    ref = ref_attention(qkv, pads, dims, window, fw, shift, heads, hd, scale, rpb)
+    err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < (2e-2 if dt == torch.bfloat16 else 1e-5), err
