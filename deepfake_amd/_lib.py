@@ -34,7 +34,8 @@ class GemmArgs(C.Structure):
 class WattnArgs(C.Structure):
     _fields_ = [("q", C.c_void_p), ("k", C.c_void_p), ("v", C.c_void_p), ("out", C.c_void_p),
                 ("rpb", C.c_void_p), ("pad_q", C.c_void_p), ("pad_k", C.c_void_p), ("pad_v", C.c_void_p),
-                ("lse", C.c_void_p), ("ld_qkv", C.c_int64), ("ld_out", C.c_int64),
+                ("lse", C.c_void_p), ("mask", C.c_void_p), ("mask_nw", C.c_int64),
+                ("ld_qkv", C.c_int64), ("ld_out", C.c_int64),
                 ("B", C.c_int32), ("D", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
                 ("wd", C.c_int32), ("wh", C.c_int32), ("ww", C.c_int32),
                 ("fd", C.c_int32), ("fh", C.c_int32), ("fw", C.c_int32),
@@ -44,7 +45,15 @@ class WattnArgs(C.Structure):
 
 class WattnBwdArgs(C.Structure):
     _fields_ = [("f", WattnArgs), ("dout", C.c_void_p), ("dq", C.c_void_p), ("dk", C.c_void_p),
-                ("dv", C.c_void_p), ("drpb", C.c_void_p), ("ld_dqkv", C.c_int64), ("ld_dout", C.c_int64)]
+                ("dv", C.c_void_p), ("drpb", C.c_void_p), ("dpad_q", C.c_void_p), ("dpad_k", C.c_void_p),
+                ("dpad_v", C.c_void_p), ("ld_dqkv", C.c_int64), ("ld_dout", C.c_int64)]
+
+
+class Im2colArgs(C.Structure):
+    _fields_ = [("sb", C.c_int64), ("sc", C.c_int64), ("st", C.c_int64), ("sh", C.c_int64), ("sw", C.c_int64),
+                ("B", C.c_int32), ("cin", C.c_int32), ("T", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
+                ("pd", C.c_int32), ("ph", C.c_int32), ("pw", C.c_int32),
+                ("Do", C.c_int32), ("Ho", C.c_int32), ("Wo", C.c_int32)]
 
 
 # (name, restype, argtypes) for every exported symbol of include/dfk.h
@@ -56,6 +65,12 @@ SIGNATURES = {
     "dfk_layernorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, C.c_int, C.c_int, _VP],
     "dfk_wattn_fwd": [C.POINTER(WattnArgs), _VP],
     "dfk_wattn_bwd": [C.POINTER(WattnBwdArgs), _VP],
+    "dfk_patch_im2col": [_VP, C.c_int, _VP, C.c_int, C.POINTER(Im2colArgs), _VP],
+    "dfk_patch_merge": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],
+    "dfk_rowmean": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],
+    "dfk_cast": [_VP, C.c_int, _VP, C.c_int, _I64, _VP],
+    "dfk_gelu_bwd": [_VP, _VP, _VP, _I64, C.c_int, _VP],
+    "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP],
 }
 
 _lib = None

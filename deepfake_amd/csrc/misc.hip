@@ -1,0 +1,212 @@
+// Data-movement kernels around the GEMMs: patch im2col (Conv3d/Conv2d with
+// kernel == stride), PatchMerging 2x2 gather / scatter, per-clip row means,
+// dtype casts and the fused SGD step.  All HBM-bound, 16-B vectorised where
+// the layout allows.
+#include "common.h"
+
+namespace {
+
+// out[row][k], row = ((b*Do+d)*Ho+h)*Wo+w, k = ((c*pd+kd)*ph+kh)*pw+kw ; zero beyond the input (pad)
+template <typename TI, typename TO>
+__global__ void im2col_kernel(const TI* __restrict__ x, TO* __restrict__ out, dfk_im2col_args a, long total) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int K = a.cin * a.pd * a.ph * a.pw;
+  const long row = idx / K;
+  const int k = (int)(idx - row * K);
+  const int kw = k % a.pw, kh = (k / a.pw) % a.ph, kd = (k / (a.pw * a.ph)) % a.pd, c = k / (a.pw * a.ph * a.pd);
+  const int w = (int)(row % a.Wo), h = (int)((row / a.Wo) % a.Ho), d = (int)((row / ((long)a.Wo * a.Ho)) % a.Do);
+  const long b = row / ((long)a.Wo * a.Ho * a.Do);
+  const int t = d * a.pd + kd, y = h * a.ph + kh, xx = w * a.pw + kw;
+  float v = 0.f;
+  if (t < a.T && y < a.H && xx < a.W) v = ldf<TI>(x + b * a.sb + c * a.sc + t * a.st + (long)y * a.sh + (long)xx * a.sw);
+  stf<TO>(out + idx, v);
+}
+
+// PatchMerging (video_swin_transformer.py:300-311 / swin_transformer2d.py:349-358):
+// out[(b,d,h2,w2)][q*C + c] = x[b,d,2h2+i,2w2+j,c], (i,j) = (0,0),(1,0),(0,1),(1,1) for q = 0..3
+template <typename T>
+__global__ void merge_kernel(const T* __restrict__ src, T* __restrict__ dst, int B, int D, int H, int W, int C,
+                             int reverse, long total_vec) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total_vec) return;
+  constexpr int VEC = 16 / sizeof(T);
+  const int H2 = (H + 1) / 2, W2 = (W + 1) / 2;
+  const int cv = C / VEC;
+  const int c = (int)(idx % cv) * VEC;
+  long r = idx / cv;
+  const int q = (int)(r % 4);
+  r /= 4;  // merged row
+  const int w2 = (int)(r % W2), h2 = (int)((r / W2) % H2);
+  const long bd = r / ((long)W2 * H2);
+  const int i = q & 1, j = q >> 1;
+  const int h = 2 * h2 + i, w = 2 * w2 + j;
+  const bool ok = h < H && w < W;
+  const long xoff = ((bd * H + h) * W + w) * C + c;
+  const long moff = r * 4L * C + (long)q * C + c;
+  if (!reverse) {
+    *reinterpret_cast<uint4*>(dst + moff) = ok ? *reinterpret_cast<const uint4*>(src + xoff) : make_uint4(0, 0, 0, 0);
+  } else if (ok) {
+    *reinterpret_cast<uint4*>(dst + xoff) = *reinterpret_cast<const uint4*>(src + moff);
+  }
+}
+
+// out[g][c] = mean_r x[g*R + r][c]   (fp32 accumulation)
+template <typename T, typename TO>
+__global__ void rowmean_kernel(const T* __restrict__ x, TO* __restrict__ out, int R, int C) {
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const T* p = x + (long)g * R * C + c;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += ldf<T>(p + (long)r * C);
+  stf<TO>(out + (long)g * C + c, s / R);
+}
+
+template <typename T>
+__global__ void gelu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ pre, T* __restrict__ dx, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) stf<T>(dx + i, ldf<T>(dy + i) * dgelu_f(ldf<T>(pre + i)));
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) stf<TO>(y + i, ldf<TI>(x + i));
+}
+
+// torch.optim.SGD semantics (momentum, dampening 0, weight decay, no nesterov):
+//   g = grad + wd*p ; buf = first ? g : mom*buf + g ; p -= lr*buf ; shadow = bf16(p)
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ grad, float* __restrict__ buf,
+                           bf16raw* __restrict__ shadow, long n, const float* __restrict__ lr_dev, float lr_host,
+                           float mom, float wd, int first) {
+  const long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i0 >= n) return;
+  const float lr = lr_dev ? *lr_dev : lr_host;
+  if (i0 + 4 <= n) {
+    float4 pv = *reinterpret_cast<float4*>(p + i0);
+    const float4 gv = *reinterpret_cast<const float4*>(grad + i0);
+    float4 bv = first ? make_float4(0, 0, 0, 0) : *reinterpret_cast<float4*>(buf + i0);
+    float* pp = reinterpret_cast<float*>(&pv);
+    const float* gg = reinterpret_cast<const float*>(&gv);
+    float* bb = reinterpret_cast<float*>(&bv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float g = gg[k] + wd * pp[k];
+      bb[k] = first ? g : mom * bb[k] + g;
+      pp[k] -= lr * bb[k];
+    }
+    *reinterpret_cast<float4*>(p + i0) = pv;
+    *reinterpret_cast<float4*>(buf + i0) = bv;
+    if (shadow) {
+      uint2 u;
+      bf16raw* e = reinterpret_cast<bf16raw*>(&u);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) e[k] = f2bf(pp[k]);
+      *reinterpret_cast<uint2*>(shadow + i0) = u;
+    }
+  } else {
+    for (long i = i0; i < n; ++i) {
+      const float g = grad[i] + wd * p[i];
+      buf[i] = first ? g : mom * buf[i] + g;
+      p[i] -= lr * buf[i];
+      if (shadow) shadow[i] = f2bf(p[i]);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int dfk_patch_im2col(const void* x, int x_dtype, void* out, int out_dtype, const dfk_im2col_args* a,
+                                hipStream_t s) {
+  if (!x || !out || !a || a->pd <= 0 || a->ph <= 0 || a->pw <= 0) return DFK_EINVAL;
+  const long rows = (long)a->B * a->Do * a->Ho * a->Wo;
+  const long total = rows * a->cin * a->pd * a->ph * a->pw;
+  if (total <= 0) return 0;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (x_dtype == DFK_F32 && out_dtype == DFK_BF16)
+    hipLaunchKernelGGL((im2col_kernel<float, bf16raw>), grid, dim3(256), 0, s, (const float*)x, (bf16raw*)out, *a, total);
+  else if (x_dtype == DFK_F32 && out_dtype == DFK_F32)
+    hipLaunchKernelGGL((im2col_kernel<float, float>), grid, dim3(256), 0, s, (const float*)x, (float*)out, *a, total);
+  else if (x_dtype == DFK_BF16 && out_dtype == DFK_BF16)
+    hipLaunchKernelGGL((im2col_kernel<bf16raw, bf16raw>), grid, dim3(256), 0, s, (const bf16raw*)x, (bf16raw*)out, *a,
+                       total);
+  else
+    return DFK_EINVAL;
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_patch_merge(const void* src, void* dst, int B, int D, int H, int W, int C, int reverse, int dtype,
+                               hipStream_t s) {
+  const int vec = dtype == DFK_BF16 ? 8 : 4;
+  if (!src || !dst || C % vec) return DFK_EINVAL;
+  const long rows = (long)B * D * ((H + 1) / 2) * ((W + 1) / 2);
+  const long total = rows * 4 * (C / vec);
+  if (total <= 0) return 0;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (dtype == DFK_BF16)
+    hipLaunchKernelGGL(merge_kernel<bf16raw>, grid, dim3(256), 0, s, (const bf16raw*)src, (bf16raw*)dst, B, D, H, W, C,
+                       reverse, total);
+  else
+    hipLaunchKernelGGL(merge_kernel<float>, grid, dim3(256), 0, s, (const float*)src, (float*)dst, B, D, H, W, C,
+                       reverse, total);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_rowmean(const void* x, void* out, int groups, int R, int C, int dtype, int out_f32, hipStream_t s) {
+  if (!x || !out || R <= 0) return DFK_EINVAL;
+  const dim3 grid(dfk_cdiv(C, 256), groups);
+  if (dtype == DFK_BF16) {
+    if (out_f32) hipLaunchKernelGGL((rowmean_kernel<bf16raw, float>), grid, dim3(256), 0, s, (const bf16raw*)x, (float*)out, R, C);
+    else hipLaunchKernelGGL((rowmean_kernel<bf16raw, bf16raw>), grid, dim3(256), 0, s, (const bf16raw*)x, (bf16raw*)out, R, C);
+  } else {
+    hipLaunchKernelGGL((rowmean_kernel<float, float>), grid, dim3(256), 0, s, (const float*)x, (float*)out, R, C);
+  }
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, int dtype, hipStream_t s) {
+  if (!dy || !pre || !dx) return DFK_EINVAL;
+  if (n <= 0) return 0;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (dtype == DFK_BF16)
+    hipLaunchKernelGGL(gelu_bwd_kernel<bf16raw>, grid, dim3(256), 0, s, (const bf16raw*)dy, (const bf16raw*)pre,
+                       (bf16raw*)dx, (long)n);
+  else
+    hipLaunchKernelGGL(gelu_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)dy, (const float*)pre, (float*)dx,
+                       (long)n);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, hipStream_t s) {
+  if (!x || !y) return DFK_EINVAL;
+  if (n <= 0) return 0;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (x_dtype == DFK_F32 && y_dtype == DFK_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16raw>), grid, dim3(256), 0, s, (const float*)x, (bf16raw*)y, (long)n);
+  else if (x_dtype == DFK_BF16 && y_dtype == DFK_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16raw, float>), grid, dim3(256), 0, s, (const bf16raw*)x, (float*)y, (long)n);
+  else
+    return DFK_EINVAL;
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow, int64_t n,
+                            const float* lr_dev, float lr, float momentum, float weight_decay, int first_step,
+                            hipStream_t s) {
+  if (!param || !grad || !momentum_buf) return DFK_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
+       reinterpret_cast<uintptr_t>(momentum_buf)) & 15)
+    return DFK_EINVAL;
+  if (n <= 0) return 0;
+  const long threads = (n + 3) / 4;
+  hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, param, grad, momentum_buf,
+                     (bf16raw*)bf16_shadow, (long)n, lr_dev, lr, momentum, weight_decay, first_step);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}

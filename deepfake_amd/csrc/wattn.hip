@@ -67,8 +67,6 @@ __device__ __forceinline__ uint4 ld16(const T* p) {
   return p ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
 }
 
-template <typename T> struct LdsLayout;
-
 // ---------------------------------------------------------------- forward
 template <typename T, int HD>
 __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, const Geo g, int qsplit) {
@@ -88,6 +86,7 @@ __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, 
   const int head = unit % a.heads;
   unit /= a.heads;
   const int win = unit % g.nW, b = unit / g.nW;
+  const float* mrow = a.mask ? a.mask + (((long)b * g.nW + win) % a.mask_nw) * g.N * g.N : nullptr;
 
   for (int i = tid; i < g.Np; i += 256) tok[i] = token_info(a, g, b, win, i);
   if (a.rpb)
@@ -154,6 +153,7 @@ __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, 
             float v = s[h2][r] * a.scale;
             if (a.rpb) v += rpb[tq.pos - tk.pos + g.C0];
             if (g.use_mask && tq.lab != tk.lab) v -= 100.f;
+            if (mrow && q < g.N && k < g.N) v += mrow[q * g.N + k];
             if (tk.row == -2) v = -INFINITY;
             s[h2][r] = v;
             bm = fmaxf(bm, v);
@@ -208,6 +208,7 @@ __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, 
             float v = s[h2][r] * a.scale;
             if (a.rpb) v += rpb[tq.pos - tk.pos + g.C0];
             if (g.use_mask && tq.lab != tk.lab) v -= 100.f;
+            if (mrow && q < g.N && k < g.N) v += mrow[q * g.N + k];
             if (tk.row == -2) v = -INFINITY;
             s[h2][r] = v;
             bm = fmaxf(bm, v);
@@ -275,7 +276,9 @@ Geo make_geo(const dfk_wattn_args& a) {
 bool args_ok(const dfk_wattn_args& a) {
   if (!a.q || !a.k || !a.v || !a.out) return false;
   if (a.hd != 32 && a.hd != 64) return false;
-  if (a.wd <= 0 || a.wh <= 0 || a.ww <= 0 || a.wd > a.fd || a.wh > a.fh || a.ww > a.fw) return false;
+  if (a.mask && a.mask_nw <= 0) return false;
+  if (a.wd <= 0 || a.wh <= 0 || a.ww <= 0 || a.fd <= 0 || a.fh <= 0 || a.fw <= 0) return false;
+  if (a.wd * a.wh * a.ww > a.fd * a.fh * a.fw) return false;  // tokens decode inside the full window (Q3)
   if (a.sd < 0 || a.sh < 0 || a.sw < 0 || a.sd >= a.wd || a.sh >= a.wh || a.sw >= a.ww) return false;
   const int vec = a.dtype == DFK_BF16 ? 8 : 4;
   if (a.ld_qkv % vec || a.ld_out % vec) return false;
@@ -317,7 +320,322 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
   return 0;
 }
 
-extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* ap, hipStream_t s) {
-  (void)ap; (void)s;
-  return DFK_EINVAL;  // TODO(round1): backward kernel
+// ---------------------------------------------------------------- backward
+// One workgroup = one (clip, window, head).  Waves own 32-key blocks with the
+// KEY on the MFMA lane: S = Q K^T and dP = dO V^T come out as [q rows][k lane]
+// accumulators, which are directly the A operand of dV = P^T dO and
+// dK = dS^T Q (X^T.B form), so dK/dV stay in registers for the whole sweep
+// over queries.  dS crosses LDS once (per-wave scratch) for dQ = dS K, which
+// all waves add into an fp32 LDS accumulator; dRPB is an LDS fp32 table
+// flushed with one global atomic per entry.
+namespace {
+
+template <typename T, int HD>
+__global__ __launch_bounds__(256) void wattn_bwd_kernel(const dfk_wattn_bwd_args ba, const Geo g, int q0, int Qn,
+                                                        int accum_kv) {
+  // queries [q0, q0+Qn) of every window are handled by this launch (Qn % 32 == 0);
+  // larger windows in fp32 run as several launches with dK/dV accumulated (accum_kv).
+  constexpr bool BF = sizeof(T) == 2;
+  const dfk_wattn_args& a = ba.f;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Lal = (g.L + 3) & ~3;
+  char* p = smem;
+  TokInfo* tok = reinterpret_cast<TokInfo*>(p); p += sizeof(TokInfo) * g.Np;
+  float* rpb = reinterpret_cast<float*>(p); p += 4 * Lal;
+  float* drpb = reinterpret_cast<float*>(p); p += 4 * Lal;
+  float* lse = reinterpret_cast<float*>(p); p += 4 * Qn;
+  float* delta = reinterpret_cast<float*>(p); p += 4 * Qn;
+  float* dQacc = reinterpret_cast<float*>(p); p += 4 * (size_t)Qn * HD;
+  T* Qs = reinterpret_cast<T*>(p); p += sizeof(T) * (size_t)Qn * HD;
+  T* dOs = reinterpret_cast<T*>(p); p += sizeof(T) * (size_t)Qn * HD;
+  T* Sd = reinterpret_cast<T*>(p);  // 4 waves x [32 q][32 k]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = lane >> 4, ql = lane & 15;
+  int unit = blockIdx.x;
+  const int head = unit % a.heads;
+  unit /= a.heads;
+  const int win = unit % g.nW, b = unit / g.nW;
+  const float* mrow = a.mask ? a.mask + (((long)b * g.nW + win) % a.mask_nw) * g.N * g.N : nullptr;
+  const int hoff = head * HD;
+  constexpr int VEC = 16 / sizeof(T);
+
+  for (int i = tid; i < g.Np; i += 256) tok[i] = token_info(a, g, b, win, i);
+  for (int l = tid; l < g.L; l += 256) {
+    rpb[l] = a.rpb ? a.rpb[(long)l * a.heads + head] : 0.f;
+    drpb[l] = 0.f;
+  }
+  __syncthreads();
+  // Q, dO rows -> LDS; lse; delta = rowsum(dO * O); zero dQ accumulator
+  for (int idx = tid; idx < Qn * (HD / VEC); idx += 256) {
+    const int li = idx / (HD / VEC), c = (idx % (HD / VEC)) * VEC;
+    const TokInfo t = tok[q0 + li];
+    *reinterpret_cast<uint4*>(Qs + li * HD + c) = ld16<T>(tok_ptr<T>(a.q, a.pad_q, t.row, a.ld_qkv, hoff + c));
+    const T* dop = t.row >= 0 ? reinterpret_cast<const T*>(ba.dout) + (long)t.row * ba.ld_dout + hoff + c : nullptr;
+    *reinterpret_cast<uint4*>(dOs + li * HD + c) = ld16<T>(dop);
+  }
+  for (int i = tid; i < Qn * HD; i += 256) dQacc[i] = 0.f;
+  for (int li = tid; li < Qn; li += 256) {
+    const int i = q0 + li;
+    const TokInfo t = tok[i];
+    float d = 0.f;
+    if (t.row >= 0) {
+      const T* op = reinterpret_cast<const T*>(a.out) + (long)t.row * a.ld_out + hoff;
+      const T* dop = reinterpret_cast<const T*>(ba.dout) + (long)t.row * ba.ld_dout + hoff;
+      for (int e = 0; e < HD; ++e) d += ldf<T>(op + e) * ldf<T>(dop + e);
+    }
+    delta[li] = d;
+    lse[li] = (i < g.N) ? a.lse[(long)blockIdx.x * g.Np + i] : 0.f;
+  }
+  __syncthreads();
+
+  T* Sw = Sd + wave * 32 * 32;
+  const int nkb = g.Np / 32, nqb = Qn / 32;
+  for (int kb = wave; kb < nkb; kb += 4) {
+    // own keys: B fragments of K^T and V^T (key on lane) and K in natural-k B layout for dQ
+    f32x4 dK[2][HD / 16], dV[2][HD / 16];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et) { dK[h2][et] = f32x4{0, 0, 0, 0}; dV[h2][et] = f32x4{0, 0, 0, 0}; }
+    TokInfo tk[2];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) tk[h2] = tok[kb * 32 + h2 * 16 + ql];
+
+    if constexpr (BF) {
+      bf16x8 kB[2][HD / 32], vB[2][HD / 32], kN[HD / 16];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const T* kp = tok_ptr<T>(a.k, a.pad_k, tk[h2].row, a.ld_qkv, hoff);
+        const T* vp = tok_ptr<T>(a.v, a.pad_v, tk[h2].row, a.ld_qkv, hoff);
+#pragma unroll
+        for (int es = 0; es < HD / 32; ++es) {
+          uint4 u = kp ? *reinterpret_cast<const uint4*>(kp + es * 32 + grp * 8) : make_uint4(0, 0, 0, 0);
+          kB[h2][es] = *reinterpret_cast<bf16x8*>(&u);
+          u = vp ? *reinterpret_cast<const uint4*>(vp + es * 32 + grp * 8) : make_uint4(0, 0, 0, 0);
+          vB[h2][es] = *reinterpret_cast<bf16x8*>(&u);
+        }
+      }
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const TokInfo t = tok[kb * 32 + grp * 8 + j];
+          const T* kp = tok_ptr<T>(a.k, a.pad_k, t.row, a.ld_qkv, hoff + et * 16 + ql);
+          kN[et][j] = kp ? __builtin_bit_cast(__bf16, *reinterpret_cast<const bf16raw*>(kp)) : (__bf16)0.f;
+        }
+      }
+      for (int qb = 0; qb < nqb; ++qb) {
+        float pv[2][2][4], ds[2][2][4];  // [qh][h2][r]
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const int qrow = qb * 32 + qh * 16 + ql;
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            f32x4 s = f32x4{0, 0, 0, 0}, dp = f32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int es = 0; es < HD / 32; ++es) {
+              const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + qrow * HD + es * 32 + grp * 8);
+              const bf16x8 da = *reinterpret_cast<const bf16x8*>(dOs + qrow * HD + es * 32 + grp * 8);
+              s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kB[h2][es], s, 0, 0, 0);
+              dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, vB[h2][es], dp, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int lq = qb * 32 + qh * 16 + grp * 4 + r;
+              const int q = q0 + lq;
+              const TokInfo tq = tok[q];
+              float v = s[r] * a.scale;
+              const int bidx = tq.pos - tk[h2].pos + g.C0;
+              if (a.rpb) v += rpb[bidx];
+              if (g.use_mask && tq.lab != tk[h2].lab) v -= 100.f;
+              const int kk = kb * 32 + h2 * 16 + ql;
+              if (mrow && q < g.N && kk < g.N) v += mrow[q * g.N + kk];
+              float P = (tq.row == -2 || tk[h2].row == -2) ? 0.f : __expf(v - lse[lq]);
+              const float dS = P * (dp[r] - delta[lq]);
+              pv[qh][h2][r] = P;
+              ds[qh][h2][r] = dS;
+              if (a.rpb && dS != 0.f) atomicAdd(drpb + bidx, dS);
+              Sw[(qh * 16 + grp * 4 + r) * 32 + h2 * 16 + ql] = f2bf(dS);
+            }
+          }
+        }
+        // dV[k][e] += sum_q P[q][k] dO[q][e] ; dK[k][e] += sum_q dS[q][k] Q[q][e]   (q-slot j <-> qh=j>>2, r=j&3)
+#pragma unroll
+        for (int et = 0; et < HD / 16; ++et) {
+          bf16x8 dob, qbv;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int q = qb * 32 + (j >> 2) * 16 + grp * 4 + (j & 3);
+            dob[j] = __builtin_bit_cast(__bf16, reinterpret_cast<const bf16raw*>(dOs)[q * HD + et * 16 + ql]);
+            qbv[j] = __builtin_bit_cast(__bf16, reinterpret_cast<const bf16raw*>(Qs)[q * HD + et * 16 + ql]);
+          }
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            bf16x8 pa, sa;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { pa[j] = (__bf16)pv[j >> 2][h2][j & 3]; sa[j] = (__bf16)ds[j >> 2][h2][j & 3]; }
+            dV[h2][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, dob, dV[h2][et], 0, 0, 0);
+            dK[h2][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, qbv, dK[h2][et], 0, 0, 0);
+          }
+        }
+        // dQ[q][e] += scale * sum_k dS[q][k] K[k][e]  (natural k order through the wave's scratch)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const bf16x8 sa = *reinterpret_cast<const bf16x8*>(Sw + (qh * 16 + ql) * 32 + grp * 8);
+#pragma unroll
+          for (int et = 0; et < HD / 16; ++et) {
+            f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, kN[et], f32x4{0, 0, 0, 0}, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              atomicAdd(dQacc + (qb * 32 + qh * 16 + grp * 4 + r) * HD + et * 16 + ql, acc[r] * a.scale);
+          }
+        }
+      }
+    } else {
+      float kB[2][HD / 4], vB[2][HD / 4], kN[HD / 16][8];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const T* kp = tok_ptr<T>(a.k, a.pad_k, tk[h2].row, a.ld_qkv, hoff);
+        const T* vp = tok_ptr<T>(a.v, a.pad_v, tk[h2].row, a.ld_qkv, hoff);
+#pragma unroll
+        for (int es = 0; es < HD / 4; ++es) {
+          kB[h2][es] = kp ? kp[es * 4 + grp] : 0.f;
+          vB[h2][es] = vp ? vp[es * 4 + grp] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et)
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          const TokInfo t = tok[kb * 32 + ks * 4 + grp];
+          const T* kp = tok_ptr<T>(a.k, a.pad_k, t.row, a.ld_qkv, hoff + et * 16 + ql);
+          kN[et][ks] = kp ? *kp : 0.f;
+        }
+      for (int qb = 0; qb < nqb; ++qb) {
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const int qrow = qb * 32 + qh * 16 + ql;
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            f32x4 s = f32x4{0, 0, 0, 0}, dp = f32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int es = 0; es < HD / 4; ++es) {
+              s = __builtin_amdgcn_mfma_f32_16x16x4f32(Qs[qrow * HD + es * 4 + grp], kB[h2][es], s, 0, 0, 0);
+              dp = __builtin_amdgcn_mfma_f32_16x16x4f32(dOs[qrow * HD + es * 4 + grp], vB[h2][es], dp, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int lq = qb * 32 + qh * 16 + grp * 4 + r;
+              const int q = q0 + lq;
+              const TokInfo tq = tok[q];
+              float v = s[r] * a.scale;
+              const int bidx = tq.pos - tk[h2].pos + g.C0;
+              if (a.rpb) v += rpb[bidx];
+              if (g.use_mask && tq.lab != tk[h2].lab) v -= 100.f;
+              const int kk = kb * 32 + h2 * 16 + ql;
+              if (mrow && q < g.N && kk < g.N) v += mrow[q * g.N + kk];
+              const float P = (tq.row == -2 || tk[h2].row == -2) ? 0.f : __expf(v - lse[lq]);
+              const float dS = P * (dp[r] - delta[lq]);
+              if (a.rpb && dS != 0.f) atomicAdd(drpb + bidx, dS);
+              Sw[(qh * 16 + grp * 4 + r) * 32 + h2 * 16 + ql] = dS;
+              // dV/dK: A[i=k][slot grp <-> q] = P / dS ; B[slot][e] = dO / Q rows q
+#pragma unroll
+              for (int et = 0; et < HD / 16; ++et) {
+                dV[h2][et] = __builtin_amdgcn_mfma_f32_16x16x4f32(P, dOs[lq * HD + et * 16 + ql], dV[h2][et], 0, 0, 0);
+                dK[h2][et] = __builtin_amdgcn_mfma_f32_16x16x4f32(dS, Qs[lq * HD + et * 16 + ql], dK[h2][et], 0, 0, 0);
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+          for (int et = 0; et < HD / 16; ++et) {
+            f32x4 acc = f32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks)
+              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Sw[(qh * 16 + ql) * 32 + ks * 4 + grp], kN[et][ks], acc, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              atomicAdd(dQacc + (qb * 32 + qh * 16 + grp * 4 + r) * HD + et * 16 + ql, acc[r] * a.scale);
+          }
+      }
+    }
+    // write dK (scaled) and dV for the 32 owned keys: C layout col = e (lane), row = key 4g+r
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = kb * 32 + h2 * 16 + grp * 4 + r;
+        const TokInfo t = tok[k];
+#pragma unroll
+        for (int et = 0; et < HD / 16; ++et) {
+          const int e = hoff + et * 16 + ql;
+          const float vk = dK[h2][et][r] * a.scale, vv = dV[h2][et][r];
+          if (t.row >= 0) {
+            T* pk = reinterpret_cast<T*>(ba.dk) + (long)t.row * ba.ld_dqkv + e;
+            T* pv = reinterpret_cast<T*>(ba.dv) + (long)t.row * ba.ld_dqkv + e;
+            stf<T>(pk, accum_kv ? ldf<T>(pk) + vk : vk);
+            stf<T>(pv, accum_kv ? ldf<T>(pv) + vv : vv);
+          } else if (t.row == -1) {
+            if (ba.dpad_k) atomicAdd(ba.dpad_k + e, vk);
+            if (ba.dpad_v) atomicAdd(ba.dpad_v + e, vv);
+          }
+        }
+      }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < Qn * HD; idx += 256) {
+    const int li = idx / HD, e = idx % HD;
+    const int i = q0 + li;
+    if (i >= g.N) continue;
+    const TokInfo t = tok[i];
+    if (t.row >= 0) stf<T>(reinterpret_cast<T*>(ba.dq) + (long)t.row * ba.ld_dqkv + hoff + e, dQacc[idx]);
+    else if (t.row == -1 && ba.dpad_q) atomicAdd(ba.dpad_q + hoff + e, dQacc[idx]);
+  }
+  if (ba.drpb)
+    for (int l = tid; l < g.L; l += 256)
+      if (drpb[l] != 0.f) atomicAdd(ba.drpb + (long)l * a.heads + head, drpb[l]);
+}
+
+// LDS bytes for a query chunk of Qn rows
+size_t bwd_lds(const dfk_wattn_args& a, const Geo& g, int Qn) {
+  const size_t es = a.dtype == DFK_BF16 ? 2 : 4;
+  const size_t Lal = (g.L + 3) & ~3;
+  return sizeof(TokInfo) * g.Np + 8 * Lal + 8 * (size_t)Qn + 4 * (size_t)Qn * a.hd + 2 * es * (size_t)Qn * a.hd +
+         es * 4 * 32 * 32;
+}
+
+}  // namespace
+
+extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
+  if (!bp || !args_ok(bp->f) || !bp->f.lse || !bp->dout || !bp->dq || !bp->dk || !bp->dv) return DFK_EINVAL;
+  const dfk_wattn_args& a = bp->f;
+  const int vec = a.dtype == DFK_BF16 ? 8 : 4;
+  if (bp->ld_dqkv % vec || bp->ld_dout % vec) return DFK_EINVAL;
+  const Geo g = make_geo(a);
+  // largest query chunk (multiple of 32) that fits the 160 KiB LDS
+  int Qn = g.Np;
+  while (Qn > 32 && bwd_lds(a, g, Qn) > 160 * 1024) Qn -= 32;
+  const size_t lds = bwd_lds(a, g, Qn);
+  if (lds > 160 * 1024) return DFK_EINVAL;
+  const long units = (long)a.B * g.nW * a.heads;
+  if (units <= 0) return 0;
+  dim3 grid((unsigned)units);
+#define LAUNCH_B(T, HD)                                                                                 \
+  do {                                                                                                  \
+    auto kfn = wattn_bwd_kernel<T, HD>;                                                                 \
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    for (int q0 = 0; q0 < g.Np; q0 += Qn)                                                               \
+      hipLaunchKernelGGL(kfn, grid, dim3(256), lds, s, *bp, g, q0, std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0); \
+  } while (0)
+  if (a.dtype == DFK_BF16) {
+    if (a.hd == 32) LAUNCH_B(bf16raw, 32); else LAUNCH_B(bf16raw, 64);
+  } else {
+    if (a.hd == 32) LAUNCH_B(float, 32); else LAUNCH_B(float, 64);
+  }
+#undef LAUNCH_B
+  DFK_CHECK_LAUNCH();
+  return 0;
 }

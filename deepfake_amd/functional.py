@@ -1,0 +1,224 @@
+"""Autograd functions over the HIP kernels (no CPU fallback: inputs must be on
+the HIP device).  Parameters stay fp32 (the reference's state_dict dtype);
+compute runs in the activation dtype (fp32 parity mode or bf16): weights are
+read through ``compute_weight`` (the bf16 shadow kept by
+deepfake_amd.params.ParamStore, else a per-call cast) and every weight /
+bias gradient is produced in fp32.
+"""
+import torch
+
+from . import kernels as K
+
+
+def compute_weight(p, dtype):
+    """Weight in the compute dtype: the parameter itself (fp32) or its bf16 shadow."""
+    if p is None:
+        return None
+    if p.dtype == dtype:
+        return p
+    sh = getattr(p, "_dfk_shadow", None)
+    if sh is not None and sh.dtype == dtype:
+        return sh
+    return p.detach().to(dtype)
+
+
+def _f32_zeros(p):
+    return torch.zeros(p.shape, device=p.device, dtype=torch.float32)
+
+
+def rows2d(x):
+    return x.reshape(-1, x.shape[-1])
+
+
+class LinearFn(torch.autograd.Function):
+    """y = x W^T + b (act 1: y = gelu(.)) (+ residual).  nn.Linear / F.linear."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, act, residual):
+        dt = x.dtype
+        w = compute_weight(weight, dt)
+        b = compute_weight(bias, dt)
+        aux = torch.empty(x.shape[0], weight.shape[0], device=x.device, dtype=dt) if act == 1 else None
+        y = K.linear(x, w, b, act=act, aux=aux, residual=residual)
+        ctx.save_for_backward(x, weight, aux)
+        ctx.act, ctx.has_bias, ctx.has_res = act, bias is not None, residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, aux = ctx.saved_tensors
+        dy = dy.contiguous()
+        dz = K.gelu_bwd(dy, aux) if ctx.act == 1 else dy
+        w = compute_weight(weight, x.dtype)
+        dx = K.linear_dx(dz, w) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = _f32_zeros(weight)
+            K.linear_dw(dz, x, dw)
+        db = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = torch.zeros(weight.shape[0], device=x.device, dtype=torch.float32)
+            K.colsum(dz, db)
+        return dx, dw, db, None, (dy if ctx.has_res else None)
+
+
+def linear(x, weight, bias=None, act=0, residual=None):
+    shp = x.shape
+    y = LinearFn.apply(rows2d(x).contiguous(), weight, bias, act,
+                       rows2d(residual).contiguous() if residual is not None else None)
+    return y.view(*shp[:-1], weight.shape[0])
+
+
+class MlpFn(torch.autograd.Function):
+    """residual + fc2(gelu(fc1(x))) — src/utils.py:242-260 Mlp (dropout 0) fused
+    with the block residual (video_swin_transformer.py:276)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, residual):
+        dt = x.dtype
+        W1, B1, W2, B2 = (compute_weight(t, dt) for t in (w1, b1, w2, b2))
+        pre = torch.empty(x.shape[0], w1.shape[0], device=x.device, dtype=dt)
+        h = K.linear(x, W1, B1, act=1, aux=pre)
+        y = K.linear(h, W2, B2, residual=residual)
+        ctx.save_for_backward(x, w1, w2, pre, h)
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w1, w2, pre, h = ctx.saved_tensors
+        dy = dy.contiguous()
+        dt = x.dtype
+        dpre = K.linear_dx(dy, compute_weight(w2, dt), act=2, aux=pre)      # (dy W2) * gelu'(pre)
+        dw2 = _f32_zeros(w2)
+        K.linear_dw(dy, h, dw2)
+        db2 = torch.zeros(w2.shape[0], device=x.device)
+        K.colsum(dy, db2)
+        dx = K.linear_dx(dpre, compute_weight(w1, dt)) if ctx.needs_input_grad[0] else None
+        dw1 = _f32_zeros(w1)
+        K.linear_dw(dpre, x, dw1)
+        db1 = torch.zeros(w1.shape[0], device=x.device)
+        K.colsum(dpre, db1)
+        return dx, dw1, db1, dw2, db2, (dy if ctx.has_res else None)
+
+
+def mlp(x, fc1, fc2, residual=None):
+    shp = x.shape
+    y = MlpFn.apply(rows2d(x).contiguous(), fc1.weight, fc1.bias, fc2.weight, fc2.bias,
+                    rows2d(residual).contiguous() if residual is not None else None)
+    return y.view(*shp[:-1], fc2.weight.shape[0])
+
+
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        dt = x.dtype
+        y, mean, rstd = K.layernorm_fwd(x, compute_weight(weight, dt), compute_weight(bias, dt), eps)
+        ctx.save_for_backward(x, weight, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, mean, rstd = ctx.saved_tensors
+        dw = torch.zeros(weight.shape, device=x.device)
+        db = torch.zeros(weight.shape, device=x.device)
+        dx = K.layernorm_bwd(dy.contiguous(), x, compute_weight(weight, x.dtype), mean, rstd, dw, db)
+        return dx, dw, db, None
+
+
+def layer_norm(x, ln):
+    shp = x.shape
+    return LayerNormFn.apply(rows2d(x).contiguous(), ln.weight, ln.bias, ln.eps).view(shp)
+
+
+class WindowAttnFn(torch.autograd.Function):
+    """Window attention core on a token-major qkv buffer [rows, 3C]
+    (video_swin_transformer.py:148-170 + forward_part1's pad/roll/partition
+    :224-252).  Inputs: qkv, rpb table [L,nH] (fp32 param or None), qkv bias
+    [3C] (the padded positions' q/k/v, or None), explicit mask or None."""
+
+    @staticmethod
+    def forward(ctx, qkv, rpb, qkv_bias, mask, geo):
+        dims, window, full_window, shift, heads, hd, scale = geo
+        C = heads * hd
+        pads = None
+        if qkv_bias is not None:
+            bc = compute_weight(qkv_bias, qkv.dtype)
+            pads = (bc[:C], bc[C:2 * C], bc[2 * C:])
+        rpb_f = rpb.detach().float().contiguous() if rpb is not None else None
+        out, lse = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], qkv.stride(0), dims, window, full_window, shift, heads,
+                               hd, scale, rpb=rpb_f, pads=pads, mask=mask)
+        ctx.save_for_backward(qkv, out, lse, rpb_f, mask)
+        ctx.pads, ctx.geo = pads, geo
+        ctx.has_rpb, ctx.has_bias = rpb is not None, qkv_bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse, rpb_f, mask = ctx.saved_tensors
+        dims, window, full_window, shift, heads, hd, scale = ctx.geo
+        C = heads * hd
+        dqkv = torch.empty_like(qkv)
+        drpb = torch.zeros_like(rpb_f) if ctx.has_rpb else None
+        dpads = [torch.zeros(C, device=qkv.device) for _ in range(3)] if ctx.has_bias else None
+        K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, qkv.stride(0), dims, window, full_window, shift, heads,
+                     hd, scale, rpb_f, ctx.pads), dout.contiguous(), dqkv, dqkv[:, C:], dqkv[:, 2 * C:], qkv.stride(0),
+                    drpb=drpb, dpads=dpads, mask=mask)
+        dbias = torch.cat(dpads) if ctx.has_bias else None
+        return dqkv, drpb, dbias, None, None
+
+
+def window_attention(qkv, rpb, qkv_bias, geo, mask=None):
+    return WindowAttnFn.apply(qkv, rpb, qkv_bias, mask, geo)
+
+
+class PatchMergeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dims):
+        ctx.dims = dims
+        return K.patch_merge(x, dims)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K.patch_merge(dy.contiguous(), ctx.dims, reverse=True), None
+
+
+class RowMeanFn(torch.autograd.Function):
+    """[groups*R, C] -> [groups, C] fp32 mean (per-clip token pooling)."""
+
+    @staticmethod
+    def forward(ctx, x, groups):
+        ctx.shape, ctx.groups, ctx.dtype = x.shape, groups, x.dtype
+        return K.rowmean(x, groups)
+
+    @staticmethod
+    def backward(ctx, dy):
+        rows, C = ctx.shape
+        R = rows // ctx.groups
+        dx = (dy / R).to(ctx.dtype)[:, None, :].expand(ctx.groups, R, C).reshape(rows, C)
+        return dx, None
+
+
+class PatchEmbedFn(torch.autograd.Function):
+    """Conv with kernel == stride as im2col + GEMM (+bias): PatchEmbed3D.proj
+    (video_swin_transformer.py:436,453) / SwinV2 PatchEmbed.proj.  Returns
+    token-major [B*Do*Ho*Wo, Cout].  No input gradient (the input is data)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, layout, patch, dtype):
+        cols, grid = K.patch_im2col(x, layout, patch, dtype)
+        W = compute_weight(weight, dtype).reshape(weight.shape[0], -1)
+        y = K.linear(cols, W, compute_weight(bias, dtype))
+        ctx.save_for_backward(cols, weight)
+        ctx.grid = grid
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, weight = ctx.saved_tensors
+        dy = dy.contiguous()
+        dw = torch.zeros(weight.shape[0], cols.shape[1], device=dy.device)
+        K.linear_dw(dy, cols, dw)
+        db = torch.zeros(weight.shape[0], device=dy.device)
+        K.colsum(dy, db)
+        return None, dw.view(weight.shape), db, None, None, None

@@ -117,8 +117,10 @@ def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False):
 
 
 def wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb=None, pads=None,
-               lse=None):
+               lse=None, mask=None):
     a = L.WattnArgs()
+    if mask is not None:
+        a.mask, a.mask_nw = mask.data_ptr(), int(mask.shape[0])
     a.q, a.k, a.v, a.out = q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
     a.rpb = rpb.data_ptr() if rpb is not None else None
     if pads is not None:
@@ -145,13 +147,99 @@ def window_geometry(dims, window):
 
 
 def wattn_fwd(q, k, v, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb=None, pads=None,
-              out=None, need_lse=True):
+              out=None, need_lse=True, mask=None):
     """Token-major window attention core; returns (out [rows, heads*hd], lse)."""
     rows = dims[0] * dims[1] * dims[2] * dims[3]
     if out is None:
         out = torch.empty(rows, heads * hd, device=q.device, dtype=q.dtype)
     nW, N, Np = window_geometry(dims, window)
     lse = torch.empty(dims[0] * nW * heads, Np, device=q.device, dtype=torch.float32) if need_lse else None
-    a = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse)
+    a = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse, mask)
     L.check(L.lib().dfk_wattn_fwd(a, L.stream()), "wattn_fwd")
     return out, lse
+
+
+def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None, mask=None):
+    """Backward of wattn_fwd.  fwd_args_tensors = (q, k, v, out, lse, ld_qkv, dims, window, full_window,
+    shift, heads, hd, scale, rpb, pads).  dq/dk/dv may alias column slices of one [rows, 3C] buffer."""
+    (q, k, v, out, lse, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads) = fwd_args_tensors
+    ba = L.WattnBwdArgs()
+    ba.f = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse, mask)
+    ba.dout = dout.data_ptr()
+    ba.dq, ba.dk, ba.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
+    ba.drpb = drpb.data_ptr() if drpb is not None else None
+    if dpads is not None:
+        ba.dpad_q, ba.dpad_k, ba.dpad_v = (p.data_ptr() for p in dpads)
+    ba.ld_dqkv = int(ld_dqkv)
+    ba.ld_dout = int(dout.stride(0))
+    L.check(L.lib().dfk_wattn_bwd(ba, L.stream()), "wattn_bwd")
+
+
+def patch_im2col(x, layout, patch, out_dtype):
+    """x: video [B,T,C,H,W] (layout 'btchw') or [B,C,T,H,W] ('bcthw') or image [B,C,H,W] ('bchw').
+    Returns (cols [B*Do*Ho*Wo, C*pd*ph*pw], (B, Do, Ho, Wo))."""
+    a = L.Im2colArgs()
+    if layout == "bchw":
+        B, Cin, H, W = x.shape
+        T = 1
+        sb, sc, sh, sw = x.stride()
+        st = 0
+        pd, ph, pw = 1, patch[0], patch[1]
+    else:
+        if layout == "btchw":
+            B, T, Cin, H, W = x.shape
+            sb, st, sc, sh, sw = x.stride()
+        else:
+            B, Cin, T, H, W = x.shape
+            sb, sc, st, sh, sw = x.stride()
+        pd, ph, pw = patch
+    Do, Ho, Wo = -(-T // pd), -(-H // ph), -(-W // pw)
+    a.sb, a.sc, a.st, a.sh, a.sw = sb, sc, st, sh, sw
+    a.B, a.cin, a.T, a.H, a.W = B, Cin, T, H, W
+    a.pd, a.ph, a.pw = pd, ph, pw
+    a.Do, a.Ho, a.Wo = Do, Ho, Wo
+    out = torch.empty(B * Do * Ho * Wo, Cin * pd * ph * pw, device=x.device, dtype=out_dtype)
+    L.check(L.lib().dfk_patch_im2col(L.ptr(x), L.dt(x), L.ptr(out), L.dt(out), a, L.stream()), "patch_im2col")
+    return out, (B, Do, Ho, Wo)
+
+
+def patch_merge(x, dims, reverse=False, out=None):
+    """dims = (B, D, H, W) of the un-merged volume; x token-major rows (or merged rows when reverse)."""
+    B, D, H, W = dims
+    C = x.shape[1] if not reverse else x.shape[1] // 4
+    if out is None:
+        if reverse:
+            out = torch.zeros(B * D * H * W, C, device=x.device, dtype=x.dtype)
+        else:
+            out = torch.empty(B * D * ((H + 1) // 2) * ((W + 1) // 2), 4 * C, device=x.device, dtype=x.dtype)
+    L.check(L.lib().dfk_patch_merge(L.ptr(x), L.ptr(out), B, D, H, W, C, int(reverse), L.dt(x), L.stream()),
+            "patch_merge")
+    return out
+
+
+def rowmean(x, groups, out_f32=True):
+    rows, C = x.shape
+    R = rows // groups
+    out = torch.empty(groups, C, device=x.device, dtype=torch.float32 if out_f32 else x.dtype)
+    L.check(L.lib().dfk_rowmean(L.ptr(x), L.ptr(out), groups, R, C, L.dt(x), int(out.dtype == torch.float32),
+                                L.stream()), "rowmean")
+    return out
+
+
+def gelu_bwd(dy, pre, out=None):
+    if out is None:
+        out = torch.empty_like(dy)
+    L.check(L.lib().dfk_gelu_bwd(L.ptr(dy), L.ptr(pre), L.ptr(out), dy.numel(), L.dt(dy), L.stream()), "gelu_bwd")
+    return out
+
+
+def cast(x, dtype):
+    y = torch.empty(x.shape, device=x.device, dtype=dtype)
+    L.check(L.lib().dfk_cast(L.ptr(x), L.dt(x), L.ptr(y), L.dt(y), x.numel(), L.stream()), "cast")
+    return y
+
+
+def sgd_step(param, grad, buf, shadow, lr, momentum, wd, first, lr_dev=None):
+    L.check(L.lib().dfk_sgd_step(L.ptr(param), L.ptr(grad), L.ptr(buf), L.ptr(shadow) if shadow is not None else None,
+                                 param.numel(), L.ptr(lr_dev) if lr_dev is not None else None, float(lr),
+                                 float(momentum), float(wd), int(first), L.stream()), "sgd_step")

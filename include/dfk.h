@@ -98,8 +98,11 @@ int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float*
  *   window (wd,wh,ww) = clamped window; full_window = RPB decode geometry (Q3);
  *   shift along each dim (0 = none); positions padded up to the window grid
  *   read the qkv bias (`pad_q/k/v`, zero input after LN, :229) .
- *   rpb: [L, nH] fp32 table or NULL;  mask: shifted-window 0/-100 mask (Q4)
- *   applied iff any shift > 0.  scale multiplies q before q k^T (Q5).
+ *   rpb: [L, nH] fp32 table or NULL;  shifted-window 0/-100 mask (Q4) from
+ *   arithmetic region labels, applied iff any shift > 0.  Alternatively an
+ *   explicit additive mask [mask_nw, N, N] fp32 (WindowAttention3D.forward's
+ *   `mask` argument, :160-163) indexed by (clip-window index) % mask_nw.
+ *   scale multiplies q before q k^T (Q5).
  *   lse (fp32 [B*nW, nH, Np]) saved for the backward. */
 typedef struct {
   const void* q; const void* k; const void* v;
@@ -107,6 +110,8 @@ typedef struct {
   const float* rpb;
   const void* pad_q; const void* pad_k; const void* pad_v;
   float* lse;
+  const float* mask;
+  int64_t mask_nw;
   int64_t ld_qkv, ld_out;
   int32_t B, D, H, W;
   int32_t wd, wh, ww;
@@ -117,15 +122,56 @@ typedef struct {
   float scale;
 } dfk_wattn_args;
 int dfk_wattn_fwd(const dfk_wattn_args* a, hipStream_t stream);
-/* backward: dq/dk/dv written at the q/k/v layout (ld_dqkv); drpb [L,nH] fp32 (+=). */
+/* backward: f is the forward's argument block (f.out = the forward output O,
+ * f.lse its log-sum-exp).  dq/dk/dv are written (=) at the q/k/v layout with
+ * row stride ld_dqkv; drpb [L,nH] fp32 (+=); gradients of padded positions
+ * (which read the qkv bias in the forward) are summed into dpad_q/k/v
+ * [heads*hd] fp32 (+=, may be NULL when the volume needs no padding). */
 typedef struct {
   dfk_wattn_args f;
   const void* dout;
   void* dq; void* dk; void* dv;
   float* drpb;
+  float* dpad_q; float* dpad_k; float* dpad_v;
   int64_t ld_dqkv, ld_dout;
 } dfk_wattn_bwd_args;
 int dfk_wattn_bwd(const dfk_wattn_bwd_args* a, hipStream_t stream);
+
+/* Patch im2col for Conv3d/Conv2d with kernel == stride (PatchEmbed3D,
+ * video_swin_transformer.py:436,446-453; SwinV2 PatchEmbed swin_transformer2d.py:461,477):
+ * out[((b*Do+d)*Ho+h)*Wo+w][((c*pd+kd)*ph+kh)*pw+kw] = x[b,c,d*pd+kd,h*ph+kh,w*pw+kw]
+ * (element strides sb..sw, so [B,T,C,H,W] clips need no permute; zero past T/H/W = F.pad). */
+typedef struct {
+  int64_t sb, sc, st, sh, sw;
+  int32_t B, cin, T, H, W;
+  int32_t pd, ph, pw;
+  int32_t Do, Ho, Wo;
+} dfk_im2col_args;
+int dfk_patch_im2col(const void* x, int x_dtype, void* out, int out_dtype, const dfk_im2col_args* a,
+                     hipStream_t stream);
+
+/* PatchMerging 2x2 gather (reverse=0) / its gradient scatter (reverse=1) on
+ * channels-last [B*D, H, W, C] <-> [B*D*ceil(H/2)*ceil(W/2), 4C], order x0,x1,x2,x3 (Q7),
+ * zero padding of odd H/W (video_swin_transformer.py:300-311). */
+int dfk_patch_merge(const void* src, void* dst, int B, int D, int H, int W, int C, int reverse, int dtype,
+                    hipStream_t stream);
+
+/* out[g][c] = mean_r x[g*R+r][c]: per-clip token means (VST mean(dim=[2,3,4]) Q8,
+ * Audio2D AdaptiveAvgPool audioTransformer.py:13,23, SwinV2 avgpool swin_transformer2d.py:614). */
+int dfk_rowmean(const void* x, void* out, int groups, int R, int C, int dtype, int out_f32, hipStream_t stream);
+
+int dfk_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, hipStream_t stream);
+
+/* dx = dy * gelu'(pre) (exact-erf GELU backward, torch nn.GELU / HF ACT2FN["gelu"]). */
+int dfk_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, int dtype, hipStream_t stream);
+
+/* torch.optim.SGD(momentum, weight_decay) step over a flat fp32 parameter
+ * buffer (src/trainer.py:80-84,295), optionally writing the bf16 compute
+ * shadow of the updated parameters in the same pass; lr read from device
+ * memory when lr_dev != NULL (graph-replay safe CosineAnnealingLR). */
+int dfk_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow, int64_t n,
+                 const float* lr_dev, float lr, float momentum, float weight_decay, int first_step,
+                 hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -66,3 +66,44 @@ def test_wattn_fwd(dt, case):
     ref = ref_attention(qkv, pads, dims, window, fw, shift, heads, hd, scale, rpb)
     err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
     assert err < (2e-2 if dt == torch.bfloat16 else 1e-5), err
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
+def test_wattn_bwd(dt, case):
+    dims, window, fw, shift, heads, hd = case
+    if False:
+        pytest.skip("fp32 (parity-mode) backward keeps the window in LDS: N <= 256 (C1 sizes)")
+    g = torch.Generator(device=DEV).manual_seed(4)
+    rows = dims[0] * dims[1] * dims[2] * dims[3]
+    C = heads * hd
+    qkv = torch.randn(rows, 3 * C, device=DEV, generator=g).to(dt)
+    pads = [0.3 * torch.randn(C, device=DEV, generator=g).to(dt) for _ in range(3)]
+    Lt = (2 * fw[0] - 1) * (2 * fw[1] - 1) * (2 * fw[2] - 1)
+    rpb = torch.randn(Lt, heads, device=DEV, generator=g) * 0.5 if hd == 32 else None
+    scale = hd ** -0.5
+    out, lse = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, window, fw, shift, heads, hd, scale,
+                           rpb=rpb, pads=pads)
+    dout = torch.randn(rows, C, device=DEV, generator=g).to(dt)
+    dqkv = torch.empty_like(qkv)
+    drpb = torch.zeros(Lt, heads, device=DEV) if rpb is not None else None
+    dpads = [torch.zeros(C, device=DEV) for _ in range(3)]
+    K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, 3 * C, dims, window, fw, shift, heads, hd, scale, rpb,
+                 pads), dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C, drpb=drpb, dpads=dpads)
+    # reference
+    qr = qkv.float().requires_grad_(True)
+    pr = [p.float().requires_grad_(True) for p in pads]
+    rr = rpb.clone().requires_grad_(True) if rpb is not None else None
+    ref = ref_attention(qr, pr, dims, window, fw, shift, heads, hd, scale, rr)
+    ref.backward(dout.float())
+    t = 3e-2 if dt == torch.bfloat16 else 1e-4
+
+    def chk(a, b, name):
+        e = ((a.float() - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+        assert e < t, f"{name}: {e}"
+    chk(dqkv, qr.grad, "dqkv")
+    if rpb is not None:
+        chk(drpb, rr.grad, "drpb")
+    padded = any(n % w for n, w in zip(dims[1:], window))
+    if padded:
+        chk(torch.cat(dpads), torch.cat([p.grad for p in pr]), "dpad")
