@@ -25,6 +25,7 @@ class GemmArgs(C.Structure):
     _fields_ = [("a", View), ("b", View), ("c", C.c_void_p), ("bias", C.c_void_p), ("residual", C.c_void_p),
                 ("aux", C.c_void_p), ("ldc", C.c_int64), ("cbs0", C.c_int64), ("cbs1", C.c_int64),
                 ("ldr", C.c_int64), ("rbs0", C.c_int64), ("rbs1", C.c_int64), ("ldaux", C.c_int64),
+                ("bias_bs1", C.c_int64),
                 ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("dtype", C.c_int32),
                 ("a_kmajor", C.c_int32), ("b_kmajor", C.c_int32), ("c_f32", C.c_int32), ("nz0", C.c_int32),
                 ("nz1", C.c_int32), ("splitk", C.c_int32), ("act", C.c_int32), ("atomic", C.c_int32),
@@ -70,6 +71,8 @@ SIGNATURES = {
     "dfk_rowmean": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],
     "dfk_cast": [_VP, C.c_int, _VP, C.c_int, _I64, _VP],
     "dfk_gelu_bwd": [_VP, _VP, _VP, _I64, C.c_int, _VP],
+    "dfk_w2v_conv0_fwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP],
+    "dfk_w2v_conv0_bwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _VP, _VP, _VP, _VP],
     "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP],
 }
 

@@ -156,10 +156,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
   }
 
   // ---- epilogue
-  const T* bias = reinterpret_cast<const T*>(g.bias);
+  const T* bias = g.bias ? reinterpret_cast<const T*>(g.bias) + z1 * g.bias_bs1 : nullptr;
   const T* res = g.residual ? reinterpret_cast<const T*>(g.residual) + z0 * g.rbs0 + z1 * g.rbs1 : nullptr;
-  T* aux = reinterpret_cast<T*>(g.aux);
   const long coff = z0 * g.cbs0 + z1 * g.cbs1;
+  T* aux = g.aux ? reinterpret_cast<T*>(g.aux) + coff : nullptr;
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi) {
 #pragma unroll

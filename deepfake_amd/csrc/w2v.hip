@@ -1,0 +1,192 @@
+// wav2vec2 feature-encoder layer 0 (HF modeling_wav2vec2.py:302-323):
+//   y[b,t,c] = sum_k w[c,k] x[b,5t+k]          Conv1d(1->512, k10, s5, no bias)
+//   z = GroupNorm(512 groups = per channel over time, affine)(y)
+//   out = gelu(z)   written channels-last [B, T0, 512] for the implicit-GEMM conv1
+// GroupNorm needs whole-time statistics per (clip, channel), so the forward is
+// two passes that both recompute the 10-tap conv from the waveform (the
+// waveform is 0.26 MB/clip; y is never stored), and the backward likewise.
+// The conv itself is VALU work (10 MACs / output) — the pass is HBM-bound on
+// the 13 MB/clip output (bf16).
+#include "common.h"
+
+namespace {
+
+constexpr int TB = 64;    // time steps per workgroup
+constexpr int CH = 512;   // channels (conv_dim[0])
+constexpr int KW = 10, KS = 5;
+
+// stage the waveform segment of this time block and the conv weights into LDS
+__device__ __forceinline__ void stage(const float* __restrict__ x, const float* __restrict__ w, long S, int b, int t0,
+                                      float* xs, float* ws) {
+  const long base = (long)b * S + (long)t0 * KS;
+  for (int i = threadIdx.x; i < TB * KS + KW; i += 256) {
+    const long j = base + i;
+    xs[i] = ((long)t0 * KS + i < S) ? x[j] : 0.f;
+  }
+  for (int i = threadIdx.x; i < CH * KW; i += 256) ws[i] = w[i];
+  __syncthreads();
+}
+
+__device__ __forceinline__ float conv_at(const float* xs, const float* ws, int tl, int c) {
+  float y = 0.f;
+#pragma unroll
+  for (int k = 0; k < KW; ++k) y += ws[c * KW + k] * xs[tl * KS + k];
+  return y;
+}
+
+// pass 1: per (b, c) sum and sum of squares of y over time (fp32 atomics)
+__global__ __launch_bounds__(256) void conv0_stats(const float* __restrict__ x, const float* __restrict__ w, long S,
+                                                   int T0, float* __restrict__ stats) {
+  __shared__ float xs[TB * KS + KW];
+  __shared__ float ws[CH * KW];
+  const int b = blockIdx.y, t0 = blockIdx.x * TB;
+  stage(x, w, S, b, t0, xs, ws);
+  const int nt = min(TB, T0 - t0);
+  for (int c = threadIdx.x; c < CH; c += 256) {
+    float s = 0.f, q = 0.f;
+    for (int tl = 0; tl < nt; ++tl) {
+      const float y = conv_at(xs, ws, tl, c);
+      s += y;
+      q += y * y;
+    }
+    atomicAdd(stats + ((long)b * CH + c) * 2, s);
+    atomicAdd(stats + ((long)b * CH + c) * 2 + 1, q);
+  }
+}
+
+// pass 2: out = gelu(gn(y)); one thread per (t, channel pair) -> coalesced channels-last stores
+template <typename T>
+__global__ __launch_bounds__(256) void conv0_apply(const float* __restrict__ x, const float* __restrict__ w, long S,
+                                                   int T0, const float* __restrict__ stats, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, float eps, T* __restrict__ out) {
+  __shared__ float xs[TB * KS + KW];
+  __shared__ float ws[CH * KW];
+  __shared__ float mu[CH], rs[CH];
+  const int b = blockIdx.y, t0 = blockIdx.x * TB;
+  stage(x, w, S, b, t0, xs, ws);
+  for (int c = threadIdx.x; c < CH; c += 256) {
+    const float s = stats[((long)b * CH + c) * 2], q = stats[((long)b * CH + c) * 2 + 1];
+    const float m = s / T0;
+    mu[c] = m;
+    rs[c] = rsqrtf(fmaxf(q / T0 - m * m, 0.f) + eps);
+  }
+  __syncthreads();
+  const int nt = min(TB, T0 - t0);
+  for (int i = threadIdx.x; i < nt * CH; i += 256) {
+    const int tl = i / CH, c = i % CH;
+    const float y = conv_at(xs, ws, tl, c);
+    const float z = (y - mu[c]) * rs[c] * gamma[c] + beta[c];
+    stf<T>(out + ((long)b * T0 + t0 + tl) * CH + c, gelu_f(z));
+  }
+}
+
+// backward pass 1: per (b,c) A = sum_t dz*yhat, Bs = sum_t dz   (dz = dout * gelu'(z))
+template <typename T>
+__global__ __launch_bounds__(256) void conv0_bwd_stats(const float* __restrict__ x, const float* __restrict__ w, long S,
+                                                       int T0, const float* __restrict__ stats,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float eps, const T* __restrict__ dout, float* __restrict__ red) {
+  __shared__ float xs[TB * KS + KW];
+  __shared__ float ws[CH * KW];
+  const int b = blockIdx.y, t0 = blockIdx.x * TB;
+  stage(x, w, S, b, t0, xs, ws);
+  const int nt = min(TB, T0 - t0);
+  for (int c = threadIdx.x; c < CH; c += 256) {
+    const float s = stats[((long)b * CH + c) * 2], q = stats[((long)b * CH + c) * 2 + 1];
+    const float m = s / T0, r = rsqrtf(fmaxf(q / T0 - m * m, 0.f) + eps);
+    float A = 0.f, Bs = 0.f;
+    for (int tl = 0; tl < nt; ++tl) {
+      const float yh = (conv_at(xs, ws, tl, c) - m) * r;
+      const float dz = ldf<T>(dout + ((long)b * T0 + t0 + tl) * CH + c) * dgelu_f(yh * gamma[c] + beta[c]);
+      A += dz * yh;
+      Bs += dz;
+    }
+    atomicAdd(red + ((long)b * CH + c) * 2, A);
+    atomicAdd(red + ((long)b * CH + c) * 2 + 1, Bs);
+  }
+}
+
+// backward pass 2: dy = rstd*(gamma*dz - gamma*Bs/T0 - yhat*gamma*A/T0);  dw[c,k] += sum_t dy x[5t+k]
+template <typename T>
+__global__ __launch_bounds__(256) void conv0_bwd_dw(const float* __restrict__ x, const float* __restrict__ w, long S,
+                                                    int T0, const float* __restrict__ stats,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    float eps, const T* __restrict__ dout, const float* __restrict__ red,
+                                                    float* __restrict__ dw) {
+  __shared__ float xs[TB * KS + KW];
+  __shared__ float ws[CH * KW];
+  const int b = blockIdx.y, t0 = blockIdx.x * TB;
+  stage(x, w, S, b, t0, xs, ws);
+  const int nt = min(TB, T0 - t0);
+  for (int c = threadIdx.x; c < CH; c += 256) {
+    const float s = stats[((long)b * CH + c) * 2], q = stats[((long)b * CH + c) * 2 + 1];
+    const float m = s / T0, r = rsqrtf(fmaxf(q / T0 - m * m, 0.f) + eps);
+    const float g = gamma[c];
+    const float A = red[((long)b * CH + c) * 2] * g / T0, Bm = red[((long)b * CH + c) * 2 + 1] * g / T0;
+    float acc[KW];
+#pragma unroll
+    for (int k = 0; k < KW; ++k) acc[k] = 0.f;
+    for (int tl = 0; tl < nt; ++tl) {
+      const float yh = (conv_at(xs, ws, tl, c) - m) * r;
+      const float dz = ldf<T>(dout + ((long)b * T0 + t0 + tl) * CH + c) * dgelu_f(yh * g + beta[c]);
+      const float dy = r * (g * dz - Bm - yh * A);
+#pragma unroll
+      for (int k = 0; k < KW; ++k) acc[k] += dy * xs[tl * KS + k];
+    }
+#pragma unroll
+    for (int k = 0; k < KW; ++k) atomicAdd(dw + c * KW + k, acc[k]);
+  }
+}
+
+// dgamma[c] += sum_b A[b,c] ; dbeta[c] += sum_b Bs[b,c]
+__global__ void gn_affine_grad(const float* __restrict__ red, int B, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= CH) return;
+  float a = 0.f, bs = 0.f;
+  for (int b = 0; b < B; ++b) { a += red[((long)b * CH + c) * 2]; bs += red[((long)b * CH + c) * 2 + 1]; }
+  if (dgamma) dgamma[c] += a;
+  if (dbeta) dbeta[c] += bs;
+}
+
+}  // namespace
+
+extern "C" int dfk_w2v_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
+                                 const float* beta, float eps, float* stats, void* out, int dtype, hipStream_t s) {
+  if (!wave || !w || !gamma || !beta || !stats || !out || S < KW) return DFK_EINVAL;
+  const int T0 = (int)((S - KW) / KS + 1);
+  const dim3 grid(dfk_cdiv(T0, TB), (unsigned)B);
+  (void)hipMemsetAsync(stats, 0, sizeof(float) * B * CH * 2, s);
+  hipLaunchKernelGGL(conv0_stats, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats);
+  if (dtype == DFK_BF16)
+    hipLaunchKernelGGL(conv0_apply<bf16raw>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
+                       (bf16raw*)out);
+  else
+    hipLaunchKernelGGL(conv0_apply<float>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
+                       (float*)out);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_w2v_conv0_bwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
+                                 const float* beta, float eps, const float* stats, const void* dout, int dtype,
+                                 float* scratch, float* dw, float* dgamma, float* dbeta, hipStream_t s) {
+  if (!wave || !w || !gamma || !beta || !stats || !dout || !scratch || !dw || S < KW) return DFK_EINVAL;
+  const int T0 = (int)((S - KW) / KS + 1);
+  const dim3 grid(dfk_cdiv(T0, TB), (unsigned)B);
+  (void)hipMemsetAsync(scratch, 0, sizeof(float) * B * CH * 2, s);
+  if (dtype == DFK_BF16) {
+    hipLaunchKernelGGL(conv0_bwd_stats<bf16raw>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
+                       (const bf16raw*)dout, scratch);
+    hipLaunchKernelGGL(conv0_bwd_dw<bf16raw>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
+                       (const bf16raw*)dout, scratch, dw);
+  } else {
+    hipLaunchKernelGGL(conv0_bwd_stats<float>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
+                       (const float*)dout, scratch);
+    hipLaunchKernelGGL(conv0_bwd_dw<float>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
+                       (const float*)dout, scratch, dw);
+  }
+  if (dgamma || dbeta)
+    hipLaunchKernelGGL(gn_affine_grad, dim3(dfk_cdiv(CH, 256)), dim3(256), 0, s, scratch, (int)B, dgamma, dbeta);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}

@@ -199,6 +199,119 @@ class RowMeanFn(torch.autograd.Function):
         return dx, None
 
 
+class W2VConv0Fn(torch.autograd.Function):
+    """wav2vec2 conv layer 0: Conv1d(1->512,k10,s5) + GroupNorm(512,512) + GELU
+    (HF modeling_wav2vec2.py:302-323) -> channels-last [B, T0, 512]."""
+
+    @staticmethod
+    def forward(ctx, wave, weight, gamma, beta, eps, dtype):
+        w = weight.detach().float().reshape(512, 10).contiguous()
+        out, stats = K.w2v_conv0_fwd(wave.float().contiguous(), w, gamma.detach().float(), beta.detach().float(), eps,
+                                     dtype)
+        ctx.save_for_backward(wave, w, gamma, beta, stats)
+        ctx.eps = eps
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        wave, w, gamma, beta, stats = ctx.saved_tensors
+        dw = torch.zeros(512, 10, device=wave.device)
+        dg = torch.zeros(512, device=wave.device)
+        db = torch.zeros(512, device=wave.device)
+        K.w2v_conv0_bwd(wave.float().contiguous(), w, gamma.detach().float(), beta.detach().float(), ctx.eps, stats,
+                        dout.contiguous(), dw, dg, db)
+        return None, dw.view(512, 1, 10), dg, db, None, None
+
+
+class ConvGeluFn(torch.autograd.Function):
+    """Channels-last Conv1d(Cin->Cout, k, stride s, no bias) + GELU as an
+    implicit GEMM (HF modeling_wav2vec2.py:253-272, conv layers 1..6):
+    y[b,t,co] = gelu(sum_{kk,ci} W[co,ci,kk] x[b, s*t+kk, ci])."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride):
+        B, Tin, Cin = x.shape
+        Cout, _, k = weight.shape
+        Tout = (Tin - k) // stride + 1
+        dt = x.dtype
+        w2 = weight.detach().permute(0, 2, 1).reshape(Cout, k * Cin).to(dt).contiguous()
+        y = torch.empty(B, Tout, Cout, device=x.device, dtype=dt)
+        pre = torch.empty_like(y)
+        K.gemm(x, Cin, False, w2, k * Cin, False, Tout, Cout, k * Cin, y, Cout, dtype=K.L.dt(x), act=1, aux=pre,
+               ldaux=Cout, nz=(B, 1), a_bs=(Tin * Cin, 0), c_bs=(Tout * Cout, 0), a_conv=(Cin, stride, 0, Tin))
+        ctx.save_for_backward(x, w2, pre)
+        ctx.meta = (stride, k, Cin, Cout, Tin, Tout, weight.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w2, pre = ctx.saved_tensors
+        stride, k, Cin, Cout, Tin, Tout, wshape = ctx.meta
+        B = x.shape[0]
+        dt = K.L.dt(x)
+        dpre = K.gelu_bwd(dy.contiguous(), pre)
+        dw2 = torch.zeros(Cout, k * Cin, device=x.device)
+        tiles = -(-Cout // 128) * -(-(k * Cin) // 128)
+        K.gemm(dpre, Cout, True, x, Cin, True, Cout, k * Cin, Tout, dw2, k * Cin, dtype=dt, c_f32=True, atomic=True,
+               splitk=max(1, min(K.splitk_for(tiles * B, Tout, 128), 16)), nz=(B, 1), a_bs=(Tout * Cout, 0),
+               b_bs=(Tin * Cin, 0), b_conv=(Cin, stride, 0, Tin))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.zeros(B, Tin, Cin, device=x.device, dtype=x.dtype)
+            for kk in range(k):  # col2im: tap kk of output t lands on input row stride*t + kk
+                K.gemm(dpre, Cout, False, w2[:, kk * Cin:], k * Cin, True, Tout, Cin, Cout, dx[:, kk:], stride * Cin,
+                       dtype=dt, beta=1.0, nz=(B, 1), a_bs=(Tout * Cout, 0), c_bs=(Tin * Cin, 0))
+        dw = dw2.view(Cout, k, Cin).permute(0, 2, 1)
+        return dx, dw, None
+
+
+class PosConvFn(torch.autograd.Function):
+    """x + gelu(grouped Conv1d(C, C, k, pad k/2, groups G)(x) + b) with the last
+    output frame dropped (HF modeling_wav2vec2.py:326-380,689-690); weight is
+    the (weight-normed) conv weight [C, C/G, k].  Implicit GEMM per (clip, group)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups):
+        B, T, C = x.shape
+        Cg = C // groups
+        k = weight.shape[2]
+        pad = k // 2
+        dt = x.dtype
+        w2 = weight.detach().permute(0, 2, 1).reshape(C, k * Cg).to(dt).contiguous()  # [co][kk*Cg+ci]
+        y = torch.empty_like(x)
+        pre = torch.empty_like(x)
+        K.gemm(x, C, False, w2, k * Cg, False, T, Cg, k * Cg, y, C, dtype=K.L.dt(x), bias=compute_weight(bias, dt),
+               bias_bs1=Cg, act=1, aux=pre, ldaux=C, residual=x, ldr=C, nz=(B, groups), a_bs=(T * C, Cg),
+               b_bs=(0, Cg * k * Cg), c_bs=(T * C, Cg), r_bs=(T * C, Cg), a_conv=(Cg, 1, pad, T))
+        ctx.save_for_backward(x, weight, pre)
+        ctx.groups = groups
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, pre = ctx.saved_tensors
+        B, T, C = x.shape
+        G = ctx.groups
+        Cg = C // G
+        k = weight.shape[2]
+        dt = K.L.dt(x)
+        dy = dy.contiguous()
+        dpre = K.gelu_bwd(dy, pre)
+        db = torch.zeros(C, device=x.device)
+        K.colsum(dpre.view(-1, C), db)
+        dw2 = torch.zeros(C, k * Cg, device=x.device)
+        K.gemm(dpre, C, True, x, C, True, Cg, k * Cg, T, dw2, k * Cg, dtype=dt, c_f32=True, atomic=True,
+               splitk=2, nz=(B, G), a_bs=(T * C, Cg), b_bs=(T * C, Cg), c_bs=(0, Cg * k * Cg),
+               b_conv=(Cg, 1, k // 2, T))
+        # dx = dy + transposed conv: kernel flipped, pad k/2-1  (W3[g*Cg+ci][u*Cg+co] = W[g*Cg+co][ci][k-1-u])
+        w3 = weight.detach().view(G, Cg, Cg, k).flip(3).permute(0, 2, 3, 1).reshape(C, k * Cg).to(x.dtype).contiguous()
+        dx = dy.clone()
+        K.gemm(dpre, C, False, w3, k * Cg, False, T, Cg, k * Cg, dx, C, dtype=dt, beta=1.0, nz=(B, G),
+               a_bs=(T * C, Cg), b_bs=(0, Cg * k * Cg), c_bs=(T * C, Cg), a_conv=(Cg, 1, k // 2 - 1, T))
+        dw = dw2.view(C, k, Cg).permute(0, 2, 1)
+        return dx, dw, db, None
+
+
 class PatchEmbedFn(torch.autograd.Function):
     """Conv with kernel == stride as im2col + GEMM (+bias): PatchEmbed3D.proj
     (video_swin_transformer.py:436,453) / SwinV2 PatchEmbed.proj.  Returns

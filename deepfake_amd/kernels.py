@@ -24,9 +24,10 @@ def _view(t, ld, bs0=0, bs1=0, conv=None):
 
 def gemm(a, a_ld, a_kmajor, b, b_ld, b_kmajor, M, N, K, c, ldc, *, dtype, c_f32=False, bias=None,
          residual=None, ldr=0, aux=None, ldaux=0, act=0, beta=0.0, atomic=False, splitk=1,
-         nz=(1, 1), a_bs=(0, 0), b_bs=(0, 0), c_bs=(0, 0), r_bs=(0, 0), a_conv=None, b_conv=None):
+         nz=(1, 1), a_bs=(0, 0), b_bs=(0, 0), c_bs=(0, 0), r_bs=(0, 0), a_conv=None, b_conv=None, bias_bs1=0):
     """Raw dfk_gemm.  a/b/c are tensors (base pointers); see include/dfk.h."""
     g = L.GemmArgs()
+    g.bias_bs1 = int(bias_bs1)
     g.a = _view(a, a_ld, *a_bs, conv=a_conv)
     g.b = _view(b, b_ld, *b_bs, conv=b_conv)
     g.c = c.data_ptr()
@@ -224,6 +225,24 @@ def rowmean(x, groups, out_f32=True):
     L.check(L.lib().dfk_rowmean(L.ptr(x), L.ptr(out), groups, R, C, L.dt(x), int(out.dtype == torch.float32),
                                 L.stream()), "rowmean")
     return out
+
+
+def w2v_conv0_fwd(wave, w, gamma, beta, eps, dtype):
+    B, S = wave.shape
+    T0 = (S - 10) // 5 + 1
+    out = torch.empty(B, T0, 512, device=wave.device, dtype=dtype)
+    stats = torch.empty(B, 512, 2, device=wave.device, dtype=torch.float32)
+    L.check(L.lib().dfk_w2v_conv0_fwd(L.ptr(wave), B, S, L.ptr(w), L.ptr(gamma), L.ptr(beta), float(eps),
+                                      L.ptr(stats), L.ptr(out), L.dt(out), L.stream()), "w2v_conv0_fwd")
+    return out, stats
+
+
+def w2v_conv0_bwd(wave, w, gamma, beta, eps, stats, dout, dw, dgamma, dbeta):
+    B, S = wave.shape
+    scratch = torch.empty(B, 512, 2, device=wave.device, dtype=torch.float32)
+    L.check(L.lib().dfk_w2v_conv0_bwd(L.ptr(wave), B, S, L.ptr(w), L.ptr(gamma), L.ptr(beta), float(eps),
+                                      L.ptr(stats), L.ptr(dout), L.dt(dout), L.ptr(scratch), L.ptr(dw), L.ptr(dgamma),
+                                      L.ptr(dbeta), L.stream()), "w2v_conv0_bwd")
 
 
 def gelu_bwd(dy, pre, out=None):

@@ -1,0 +1,222 @@
+"""wav2vec2-base on MI355X with HF-compatible state_dict keys (drop-in for the
+``transformers.Wav2Vec2Model`` the reference builds at train.py:46 and wraps in
+Audio2D, audioTransformer.py:5-30).  Restates transformers 5.15.0
+models/wav2vec2/modeling_wav2vec2.py (HF/ below) on HIP kernels:
+
+  conv0 + GroupNorm + GELU        dfk_w2v_conv0_*   (HF/:302-323)
+  conv1..6 + GELU                 implicit-GEMM conv (HF/:253-272), channels-last
+  feature projection LN + Linear  (HF/:422-435)
+  weight-normed grouped pos-conv  implicit GEMM per (clip, group), + residual (HF/:326-380,689)
+  12 post-LN encoder layers       fused qkv GEMM, whole-sequence attention kernel,
+                                  out_proj+residual, LN, FFN(+residual), LN (HF/:575-608)
+
+Deterministic configuration only (dropouts, LayerDrop, SpecAugment must be 0:
+constructing for training with them raises), matching the parity setup (Q12).
+"""
+import json
+
+import torch
+import torch.nn as nn
+from torch.nn.utils import parametrizations
+
+from .. import functional as Fn
+
+
+class Wav2Vec2Config:
+    """The fields of HF Wav2Vec2Config this path reads (config.json of the
+    reference checkpoint: checkpoints/wav2vec2-base-960h/config.json)."""
+
+    def __init__(self, **kw):
+        self.conv_dim = kw.get("conv_dim", [512] * 7)
+        self.conv_kernel = kw.get("conv_kernel", [10, 3, 3, 3, 3, 2, 2])
+        self.conv_stride = kw.get("conv_stride", [5, 2, 2, 2, 2, 2, 2])
+        self.conv_bias = kw.get("conv_bias", False)
+        self.feat_extract_norm = kw.get("feat_extract_norm", "group")
+        self.hidden_size = kw.get("hidden_size", 768)
+        self.num_attention_heads = kw.get("num_attention_heads", 12)
+        self.intermediate_size = kw.get("intermediate_size", 3072)
+        self.num_hidden_layers = kw.get("num_hidden_layers", 12)
+        self.num_conv_pos_embeddings = kw.get("num_conv_pos_embeddings", 128)
+        self.num_conv_pos_embedding_groups = kw.get("num_conv_pos_embedding_groups", 16)
+        self.layer_norm_eps = kw.get("layer_norm_eps", 1e-5)
+        self.do_stable_layer_norm = kw.get("do_stable_layer_norm", False)
+        self.mask_time_prob = kw.get("mask_time_prob", 0.05)
+        self.mask_feature_prob = kw.get("mask_feature_prob", 0.0)
+        self.layerdrop = kw.get("layerdrop", 0.1)
+        for k in ("hidden_dropout", "attention_dropout", "activation_dropout", "feat_proj_dropout"):
+            setattr(self, k, kw.get(k, 0.1))
+
+    @classmethod
+    def from_json_file(cls, path, **overrides):
+        with open(path) as f:
+            d = json.load(f)
+        d.update(overrides)
+        return cls(**d)
+
+    def deterministic(self):
+        """Parity / benchmark setting (Q12): dropouts, LayerDrop and SpecAugment off."""
+        for k in ("hidden_dropout", "attention_dropout", "activation_dropout", "feat_proj_dropout", "layerdrop",
+                  "mask_time_prob", "mask_feature_prob"):
+            setattr(self, k, 0.0)
+        return self
+
+
+class _ConvLayer(nn.Module):
+    def __init__(self, cin, cout, k, s, group_norm):
+        super().__init__()
+        self.conv = nn.Conv1d(cin, cout, kernel_size=k, stride=s, bias=False)
+        if group_norm:
+            self.layer_norm = nn.GroupNorm(num_groups=cout, num_channels=cout, affine=True)
+        self.stride = s
+
+
+class Wav2Vec2FeatureEncoder(nn.Module):
+    """HF/:382-419 (feat_extract_norm == "group")."""
+
+    def __init__(self, config):
+        super().__init__()
+        if config.feat_extract_norm != "group" or config.conv_bias or config.conv_dim[0] != 512 \
+                or config.conv_kernel[0] != 10 or config.conv_stride[0] != 5:
+            raise NotImplementedError("only the wav2vec2-base feature encoder (group norm, 512x10/5 conv0)")
+        dims = [1] + list(config.conv_dim)
+        self.conv_layers = nn.ModuleList([
+            _ConvLayer(dims[i], dims[i + 1], config.conv_kernel[i], config.conv_stride[i], i == 0)
+            for i in range(len(config.conv_dim))])
+        self.compute_dtype = torch.float32
+
+    def forward(self, input_values):
+        """[B, S] fp32 -> channels-last [B, T, 512] (compute dtype)."""
+        l0 = self.conv_layers[0]
+        x = Fn.W2VConv0Fn.apply(input_values, l0.conv.weight, l0.layer_norm.weight, l0.layer_norm.bias,
+                                l0.layer_norm.eps, self.compute_dtype)
+        for layer in self.conv_layers[1:]:
+            x = Fn.ConvGeluFn.apply(x, layer.conv.weight, layer.stride)
+        return x
+
+
+class Wav2Vec2FeatureProjection(nn.Module):
+    """HF/:422-435."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.layer_norm = nn.LayerNorm(config.conv_dim[-1], eps=config.layer_norm_eps)
+        self.projection = nn.Linear(config.conv_dim[-1], config.hidden_size)
+
+    def forward(self, x):
+        n = Fn.layer_norm(x, self.layer_norm)
+        return Fn.linear(n, self.projection.weight, self.projection.bias), n
+
+
+class Wav2Vec2PositionalConvEmbedding(nn.Module):
+    """HF/:326-368 (weight-norm dim=2; SamePad drops the last frame)."""
+
+    def __init__(self, config):
+        super().__init__()
+        conv = nn.Conv1d(config.hidden_size, config.hidden_size, kernel_size=config.num_conv_pos_embeddings,
+                         padding=config.num_conv_pos_embeddings // 2, groups=config.num_conv_pos_embedding_groups)
+        self.conv = parametrizations.weight_norm(conv, name="weight", dim=2)
+        self.groups = config.num_conv_pos_embedding_groups
+        if config.num_conv_pos_embeddings % 2:
+            raise NotImplementedError("odd num_conv_pos_embeddings")
+
+    def add_to(self, x):
+        """x + pos_conv(x) fused (HF/:689-690)."""
+        return Fn.PosConvFn.apply(x, self.conv.weight, self.conv.bias, self.groups)
+
+
+class Wav2Vec2Attention(nn.Module):
+    """HF/:466-548: q/k/v/out projections; softmax(q k^T * hd^-0.5) v."""
+
+    def __init__(self, embed_dim, num_heads):
+        super().__init__()
+        self.embed_dim, self.num_heads = embed_dim, num_heads
+        self.head_dim = embed_dim // num_heads
+        self.scaling = self.head_dim ** -0.5
+        self.k_proj = nn.Linear(embed_dim, embed_dim)
+        self.v_proj = nn.Linear(embed_dim, embed_dim)
+        self.q_proj = nn.Linear(embed_dim, embed_dim)
+        self.out_proj = nn.Linear(embed_dim, embed_dim)
+
+    def core(self, x, B, T):
+        """x [B*T, C] -> attention output [B*T, C] before out_proj."""
+        w = torch.cat((self.q_proj.weight, self.k_proj.weight, self.v_proj.weight))
+        b = torch.cat((self.q_proj.bias, self.k_proj.bias, self.v_proj.bias))
+        qkv = Fn.linear(x, w, b)
+        geo = ((B, 1, 1, T), (1, 1, T), (1, 1, T), (0, 0, 0), self.num_heads, self.head_dim, self.scaling)
+        return Fn.window_attention(qkv, None, None, geo)
+
+
+class Wav2Vec2FeedForward(nn.Module):
+    """HF/:551-573."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.intermediate_dense = nn.Linear(config.hidden_size, config.intermediate_size)
+        self.output_dense = nn.Linear(config.intermediate_size, config.hidden_size)
+
+
+class Wav2Vec2EncoderLayer(nn.Module):
+    """HF/:575-608 (post-LN)."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.attention = Wav2Vec2Attention(config.hidden_size, config.num_attention_heads)
+        self.layer_norm = nn.LayerNorm(config.hidden_size, eps=config.layer_norm_eps)
+        self.feed_forward = Wav2Vec2FeedForward(config)
+        self.final_layer_norm = nn.LayerNorm(config.hidden_size, eps=config.layer_norm_eps)
+
+    def forward(self, x, B, T):
+        a = self.attention.core(x, B, T)
+        x = Fn.layer_norm(Fn.linear(a, self.attention.out_proj.weight, self.attention.out_proj.bias, residual=x),
+                          self.layer_norm)
+        ff = self.feed_forward
+        x = Fn.mlp(x, ff.intermediate_dense, ff.output_dense, residual=x)
+        return Fn.layer_norm(x, self.final_layer_norm)
+
+
+class Wav2Vec2Encoder(nn.Module):
+    """HF/:657-727 (no attention mask: equal-length clips, Q13)."""
+
+    def __init__(self, config):
+        super().__init__()
+        if config.do_stable_layer_norm:
+            raise NotImplementedError("stable-layer-norm encoder")
+        self.pos_conv_embed = Wav2Vec2PositionalConvEmbedding(config)
+        self.layer_norm = nn.LayerNorm(config.hidden_size, eps=config.layer_norm_eps)
+        self.layers = nn.ModuleList([Wav2Vec2EncoderLayer(config) for _ in range(config.num_hidden_layers)])
+
+    def forward(self, h):
+        B, T, C = h.shape
+        x = Fn.layer_norm(self.pos_conv_embed.add_to(h.contiguous()), self.layer_norm).reshape(B * T, C)
+        for layer in self.layers:
+            x = layer(x, B, T)
+        return x.view(B, T, C)
+
+
+class Wav2Vec2Model(nn.Module):
+    """HF/:1244-1380 forward (SpecAugment / LayerDrop / dropouts must be off)."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        self.feature_extractor = Wav2Vec2FeatureEncoder(config)
+        self.feature_projection = Wav2Vec2FeatureProjection(config)
+        if config.mask_time_prob > 0.0 or config.mask_feature_prob > 0.0:
+            self.masked_spec_embed = nn.Parameter(torch.empty(config.hidden_size).uniform_())
+        self.encoder = Wav2Vec2Encoder(config)
+
+    def _check_deterministic(self):
+        c = self.config
+        if self.training and (c.mask_time_prob > 0 or c.mask_feature_prob > 0 or c.layerdrop > 0 or
+                              c.hidden_dropout > 0 or c.attention_dropout > 0 or c.activation_dropout > 0 or
+                              c.feat_proj_dropout > 0):
+            raise NotImplementedError("wav2vec2 training with SpecAugment/LayerDrop/dropout > 0 is not implemented on "
+                                      "the MI355X path: use config.deterministic()")
+
+    def forward(self, input_values, attention_mask=None, **_):
+        if attention_mask is not None:
+            raise NotImplementedError("attention_mask (padded batches)")
+        self._check_deterministic()
+        f = self.feature_extractor(input_values)
+        h, ext = self.feature_projection(f)
+        return {"last_hidden_state": self.encoder(h), "extract_features": ext}

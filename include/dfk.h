@@ -62,7 +62,8 @@ typedef struct {
   void* aux;
   int64_t ldc, cbs0, cbs1;
   int64_t ldr, rbs0, rbs1;
-  int64_t ldaux;
+  int64_t ldaux;        /* aux shares C's batch strides (cbs0, cbs1) */
+  int64_t bias_bs1;     /* bias offset per z1 (grouped convs) */
   int32_t M, N, K;
   int32_t dtype;        /* of A, B, bias, residual, aux (and C unless c_f32) */
   int32_t a_kmajor, b_kmajor;
@@ -161,6 +162,19 @@ int dfk_patch_merge(const void* src, void* dst, int B, int D, int H, int W, int 
 int dfk_rowmean(const void* x, void* out, int groups, int R, int C, int dtype, int out_f32, hipStream_t stream);
 
 int dfk_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, hipStream_t stream);
+
+/* wav2vec2 feature-encoder layer 0 (HF modeling_wav2vec2.py:302-323,
+ * Wav2Vec2GroupNormConvLayer): Conv1d(1->512,k10,s5,no bias) -> GroupNorm(512,512)
+ * (per clip and channel over all T0=(S-10)/5+1 frames) -> GELU, output
+ * channels-last [B, T0, 512] (dtype).  wave [B,S] fp32, w [512,10], gamma/beta
+ * [512] fp32; stats [B,512,2] fp32 (sum, sumsq of the conv output) saved for
+ * the backward.  The conv output is recomputed, never stored. */
+int dfk_w2v_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
+                      const float* beta, float eps, float* stats, void* out, int dtype, hipStream_t stream);
+/* backward: dw [512,10], dgamma, dbeta fp32 (+=); scratch [B,512,2] fp32. */
+int dfk_w2v_conv0_bwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
+                      const float* beta, float eps, const float* stats, const void* dout, int dtype,
+                      float* scratch, float* dw, float* dgamma, float* dbeta, hipStream_t stream);
 
 /* dx = dy * gelu'(pre) (exact-erf GELU backward, torch nn.GELU / HF ACT2FN["gelu"]). */
 int dfk_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, int dtype, hipStream_t stream);

@@ -1,0 +1,104 @@
+"""GPU parity: deepfake_amd wav2vec2 (HIP path) vs the golden vectors produced by
+transformers 5.15.0's Wav2Vec2Model (2 layers, 1 s) and per-op torch fp32
+references.  Tolerances: fp32 1e-3 (the fixture is pinned at 1e-4 on CPU),
+bf16 5e-2 forward."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import golden_cases as GC
+from fixtures import check, keys, load
+from oracle.fill import named_fill_, randn, synthetic_inputs
+
+pytestmark = pytest.mark.gpu
+if torch.cuda.is_available():
+    from deepfake_amd import functional as Fn
+    from deepfake_amd.models import set_compute_dtype
+    from deepfake_amd.models import wav2vec2 as W
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv0_groupnorm_gelu(dt):
+    g = torch.Generator().manual_seed(0)
+    wave = torch.randn(2, 4000, generator=g).to(DEV)
+    w = (torch.randn(512, 1, 10, generator=g) * 0.3).to(DEV).requires_grad_(True)
+    ga = (1 + 0.1 * torch.randn(512, generator=g)).to(DEV).requires_grad_(True)
+    be = (0.1 * torch.randn(512, generator=g)).to(DEV).requires_grad_(True)
+    y = Fn.W2VConv0Fn.apply(wave, w, ga, be, 1e-5, dt)
+    ref = F.gelu(F.group_norm(F.conv1d(wave[:, None], w, stride=5), 512, ga, be, 1e-5)).transpose(1, 2)
+    t = 1e-4 if dt == torch.float32 else 2e-2
+    assert rel(y, ref) < t
+    dy = torch.randn(y.shape, generator=g).to(DEV).to(dt)
+    y.backward(dy)
+    gw, gg, gb = w.grad.clone(), ga.grad.clone(), be.grad.clone()
+    w.grad = ga.grad = be.grad = None
+    ref.backward(dy.float())
+    tb = 1e-3 if dt == torch.float32 else 3e-2
+    assert rel(gw, w.grad) < tb and rel(gg, ga.grad) < tb and rel(gb, be.grad) < tb
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("k,s,Tin", [(3, 2, 99), (3, 2, 100), (2, 2, 50), (2, 2, 49)])
+def test_conv_gelu(dt, k, s, Tin):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(3, Tin, 512, generator=g).to(DEV).to(dt).requires_grad_(True)
+    w = (torch.randn(512, 512, k, generator=g) / 40).to(DEV).requires_grad_(True)
+    y = Fn.ConvGeluFn.apply(x, w, s)
+    ref = F.gelu(F.conv1d(x.float().transpose(1, 2), w, stride=s)).transpose(1, 2)
+    t = 1e-4 if dt == torch.float32 else 2e-2
+    assert rel(y, ref) < t
+    dy = torch.randn(y.shape, generator=g).to(DEV).to(dt)
+    y.backward(dy)
+    dx, dw = x.grad.clone(), w.grad.clone()
+    xr = x.detach().float().requires_grad_(True)
+    w.grad = None
+    F.gelu(F.conv1d(xr.transpose(1, 2), w, stride=s)).transpose(1, 2).backward(dy.float())
+    tb = 1e-3 if dt == torch.float32 else 3e-2
+    assert rel(dx, xr.grad) < tb and rel(dw, w.grad) < tb
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_pos_conv(dt):
+    g = torch.Generator().manual_seed(2)
+    T = 49
+    x = torch.randn(2, T, 768, generator=g).to(DEV).to(dt).requires_grad_(True)
+    w = (torch.randn(768, 48, 128, generator=g) / 80).to(DEV).requires_grad_(True)
+    b = (0.1 * torch.randn(768, generator=g)).to(DEV).requires_grad_(True)
+    y = Fn.PosConvFn.apply(x, w, b, 16)
+    xr = x.detach().float().requires_grad_(True)
+    ref = xr + F.gelu(F.conv1d(xr.transpose(1, 2), w, b, padding=64, groups=16)[:, :, :-1]).transpose(1, 2)
+    t = 1e-4 if dt == torch.float32 else 2e-2
+    assert rel(y, ref) < t
+    dy = torch.randn(y.shape, generator=g).to(DEV).to(dt)
+    y.backward(dy)
+    dx, dw, db = x.grad.clone(), w.grad.clone(), b.grad.clone()
+    w.grad = b.grad = None
+    ref.backward(dy.float())
+    tb = 1e-3 if dt == torch.float32 else 3e-2
+    assert rel(dx, xr.grad) < tb and rel(dw, w.grad) < tb and rel(db, b.grad) < tb
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_w2v_2layer_golden(dt):
+    c = GC.W2V_C1
+    fx = load(c["name"])
+    cfg = W.Wav2Vec2Config.from_json_file(GC.W2V_CONFIG_JSON, num_hidden_layers=c["layers"]).deterministic()
+    m = named_fill_(W.Wav2Vec2Model(cfg), c["seed"]).to(DEV)
+    set_compute_dtype(m, dt)
+    _, _, wave, _ = synthetic_inputs(c["B"], 2, 16, 16, c["seconds"], seed=c["seed"] + 1)
+    out = m(wave.to(DEV))
+    h = out["last_hidden_state"]
+    h.backward(randn(c["seed"] + 2, h.shape).to(DEV).to(dt))
+    tf = 1e-3 if dt == torch.float32 else 5e-2
+    tb = 2e-3 if dt == torch.float32 else 1e-1
+    check(fx, "y", h, tf)
+    check(fx, "extract", out["extract_features"], tf)
+    names = dict(m.named_parameters())
+    for k in keys(fx, "g:"):
+        check(fx, k, names[k[2:]].grad, tb, what=f"[{k}] ")
