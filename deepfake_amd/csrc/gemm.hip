@@ -17,19 +17,40 @@ template <typename T> struct GT;
 template <> struct GT<bf16raw> { static constexpr int BK = 64, VEC = 8, PAD = 8; };
 template <> struct GT<float> { static constexpr int BK = 32, VEC = 4, PAD = 4; };
 
-// 16-byte load of VEC contiguous elements V(r, c .. c+VEC-1); zero when out of range.
-template <typename T>
-__device__ __forceinline__ uint4 view_load(const T* base, const dfk_view& v, long r, long c, bool ok) {
-  uint4 z = make_uint4(0, 0, 0, 0);
-  if (!ok) return z;
-  long row = r, col = c;
+// element offset of V(r, c), or -1 when it lies in the conv view's zero padding
+__device__ __forceinline__ long view_off(const dfk_view& v, long r, long c) {
   if (v.conv_cg > 0) {
     const long kk = c / v.conv_cg;
-    col = c - kk * v.conv_cg;
-    row = r * v.conv_stride + kk - v.conv_pad;
-    if (row < 0 || row >= v.conv_rows) return z;
+    const long row = r * v.conv_stride + kk - v.conv_pad;
+    if (row < 0 || row >= v.conv_rows) return -1;
+    return row * v.ld + (c - kk * v.conv_cg);
   }
-  return *reinterpret_cast<const uint4*>(base + row * v.ld + col);
+  return r * v.ld + c;
+}
+
+// 16-byte load of VEC contiguous elements V(r, c .. c+VEC-1); zero outside the
+// view (rok false, c >= climit, conv padding).  `vec` (host-checked alignment of
+// ptr/ld/batch strides/conv group) selects the vector load; otherwise (odd
+// shapes such as the out_dim=1 classifier) element-wise loads.
+template <typename T>
+__device__ __forceinline__ uint4 view_load(const T* base, const dfk_view& v, long r, long c, bool rok, long climit,
+                                           bool vec) {
+  constexpr int VEC = 16 / sizeof(T);
+  uint4 z = make_uint4(0, 0, 0, 0);
+  if (!rok || c >= climit) return z;
+  if (vec && c + VEC <= climit) {
+    const long o = view_off(v, r, c);
+    return o < 0 ? z : *reinterpret_cast<const uint4*>(base + o);
+  }
+  T* e = reinterpret_cast<T*>(&z);
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    if (c + i < climit) {
+      const long o = view_off(v, r, c + i);
+      if (o >= 0) e[i] = base[o];
+    }
+  }
+  return z;
 }
 
 template <typename T>
@@ -42,7 +63,7 @@ __device__ __forceinline__ void scatter_col(T* lds, int stride, int r0, int kcol
 
 template <typename T, bool KMAJ, int ROWS>
 __device__ __forceinline__ void load_tile(const T* base, const dfk_view& v, int row0, int rowlim, int k0, int klim,
-                                          int tid, uint4 (&r)[4]) {
+                                          int tid, bool vec, uint4 (&r)[4]) {
   constexpr int TBK = GT<T>::BK, VEC = GT<T>::VEC;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -50,11 +71,11 @@ __device__ __forceinline__ void load_tile(const T* base, const dfk_view& v, int 
     if (!KMAJ) {  // view rows = tile rows, contiguous along k
       const int i = idx / (TBK / VEC), kc = idx % (TBK / VEC);
       const int gr = row0 + i, gk = k0 + kc * VEC;
-      r[s] = view_load<T>(base, v, gr, gk, gr < rowlim && gk < klim);
+      r[s] = view_load<T>(base, v, gr, gk, gr < rowlim, klim, vec);
     } else {      // view rows = k, contiguous along tile rows
       const int k = idx / (ROWS / VEC), ic = idx % (ROWS / VEC);
       const int gk = k0 + k, gr = row0 + ic * VEC;
-      r[s] = view_load<T>(base, v, gk, gr, gk < klim && gr < rowlim);
+      r[s] = view_load<T>(base, v, gk, gr, gk < klim, rowlim, vec);
     }
   }
 }
@@ -78,7 +99,7 @@ __device__ __forceinline__ void store_tile(T* lds, int tid, const uint4 (&r)[4])
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 template <typename T, bool AK, bool BK>
-__global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk) {
+__global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int avec, int bvec) {
   constexpr int TBK = GT<T>::BK, S = TBK + GT<T>::PAD;
   __shared__ __attribute__((aligned(16))) T As[BM * S];
   __shared__ __attribute__((aligned(16))) T Bs[BN * S];
@@ -102,8 +123,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
 
   uint4 ra[4], rb[4];
   if (kbeg < kend) {
-    load_tile<T, AK, BM>(A, g.a, bm, g.M, kbeg, kend, tid, ra);
-    load_tile<T, BK, BN>(B, g.b, bn, g.N, kbeg, kend, tid, rb);
+    load_tile<T, AK, BM>(A, g.a, bm, g.M, kbeg, kend, tid, avec, ra);
+    load_tile<T, BK, BN>(B, g.b, bn, g.N, kbeg, kend, tid, bvec, rb);
     store_tile<T, AK, BM>(As, tid, ra);
     store_tile<T, BK, BN>(Bs, tid, rb);
   }
@@ -111,8 +132,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
   for (int k0 = kbeg; k0 < kend; k0 += TBK) {
     const bool more = k0 + TBK < kend;
     if (more) {
-      load_tile<T, AK, BM>(A, g.a, bm, g.M, k0 + TBK, kend, tid, ra);
-      load_tile<T, BK, BN>(B, g.b, bn, g.N, k0 + TBK, kend, tid, rb);
+      load_tile<T, AK, BM>(A, g.a, bm, g.M, k0 + TBK, kend, tid, avec, ra);
+      load_tile<T, BK, BN>(B, g.b, bn, g.N, k0 + TBK, kend, tid, bvec, rb);
     }
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
@@ -204,21 +225,20 @@ __global__ void colsum_kernel(const T* __restrict__ x, long rows, int cols, long
   atomicAdd(out + j, s);
 }
 
-bool view_ok(const dfk_view& v, int vec, long contig_extent) {
-  if (!v.ptr) return false;
-  if (contig_extent % vec) return false;
+// 16-byte vector loads are legal for this view (else the element-wise path runs)
+bool view_vec(const dfk_view& v, int vec) {
   if (v.ld % vec || v.bs0 % vec || v.bs1 % vec) return false;
   if ((reinterpret_cast<uintptr_t>(v.ptr) & 15) != 0) return false;
-  if (v.conv_cg > 0 && (v.conv_cg % vec || v.conv_stride <= 0)) return false;
+  if (v.conv_cg > 0 && v.conv_cg % vec) return false;
   return true;
 }
 
 template <typename T>
 int launch(const dfk_gemm_args& g, hipStream_t s) {
   constexpr int VEC = GT<T>::VEC, TBK = GT<T>::BK;
-  // contiguous extents: A !kmajor -> K, kmajor -> M ; B !kmajor -> K, kmajor -> N
-  if (!view_ok(g.a, VEC, g.a_kmajor ? g.M : g.K)) return DFK_EINVAL;
-  if (!view_ok(g.b, VEC, g.b_kmajor ? g.N : g.K)) return DFK_EINVAL;
+  if (!g.a.ptr || !g.b.ptr || !g.c) return DFK_EINVAL;
+  if ((g.a.conv_cg > 0 && g.a.conv_stride <= 0) || (g.b.conv_cg > 0 && g.b.conv_stride <= 0)) return DFK_EINVAL;
+  const int avec = view_vec(g.a, VEC), bvec = view_vec(g.b, VEC);
   if (g.splitk < 1 || g.nz0 < 1 || g.nz1 < 1) return DFK_EINVAL;
   if (g.splitk > 1 && !g.atomic) return DFK_EINVAL;
   if (g.atomic && (!g.c_f32 || g.bias || g.residual || g.act)) return DFK_EINVAL;
@@ -229,11 +249,11 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   dim3 grid(dfk_cdiv(g.N, BN), dfk_cdiv(g.M, BM), g.nz0 * g.nz1 * g.splitk);
   if (grid.y > 65535 || grid.z > 65535) return DFK_EINVAL;
   if (g.a_kmajor) {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, true, true>), grid, dim3(NT), 0, s, g, kchunk);
-    else hipLaunchKernelGGL((gemm_kernel<T, true, false>), grid, dim3(NT), 0, s, g, kchunk);
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, true, true>), grid, dim3(NT), 0, s, g, kchunk, avec, bvec);
+    else hipLaunchKernelGGL((gemm_kernel<T, true, false>), grid, dim3(NT), 0, s, g, kchunk, avec, bvec);
   } else {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, false, true>), grid, dim3(NT), 0, s, g, kchunk);
-    else hipLaunchKernelGGL((gemm_kernel<T, false, false>), grid, dim3(NT), 0, s, g, kchunk);
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, false, true>), grid, dim3(NT), 0, s, g, kchunk, avec, bvec);
+    else hipLaunchKernelGGL((gemm_kernel<T, false, false>), grid, dim3(NT), 0, s, g, kchunk, avec, bvec);
   }
   DFK_CHECK_LAUNCH();
   return 0;

@@ -115,7 +115,108 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ grad
   }
 }
 
+// SwinV2 cosine attention prologue (swin_transformer2d.py:154-157): per (row, head)
+//   q' = q / max(|q|, 1e-12) * scale[h] ;  k' = k / max(|k|, 1e-12) ;  v' = v
+template <typename T>
+__global__ void cosine_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, const float* __restrict__ scale,
+                                  long rows, int heads, int hd) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * heads) return;
+  const long r = idx / heads;
+  const int h = (int)(idx % heads);
+  const int C = heads * hd;
+  const T* q = qkv + r * 3 * C + h * hd;
+  T* o = out + r * 3 * C + h * hd;
+  float nq = 0.f, nk = 0.f;
+  for (int e = 0; e < hd; ++e) {
+    const float a = ldf<T>(q + e), b = ldf<T>(q + C + e);
+    nq += a * a;
+    nk += b * b;
+  }
+  const float iq = scale[h] / fmaxf(sqrtf(nq), 1e-12f), ik = 1.f / fmaxf(sqrtf(nk), 1e-12f);
+  for (int e = 0; e < hd; ++e) {
+    stf<T>(o + e, ldf<T>(q + e) * iq);
+    stf<T>(o + C + e, ldf<T>(q + C + e) * ik);
+    o[2 * C + e] = q[2 * C + e];
+  }
+}
+
+// backward: dq = (s*dq' - qh*(qh . s*dq'))/|q| ; dk likewise (s = 1) ; dv = dv' ; dscale[h] += qh . dq'
+template <typename T>
+__global__ void cosine_bwd_kernel(const T* __restrict__ qkv, const T* __restrict__ dout, T* __restrict__ dqkv,
+                                  const float* __restrict__ scale, float* __restrict__ dscale, long rows, int heads,
+                                  int hd) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  float ds = 0.f;
+  int h = 0;
+  if (idx < rows * heads) {
+    const long r = idx / heads;
+    h = (int)(idx % heads);
+    const int C = heads * hd;
+    const long base = r * 3 * C + h * hd;
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      const T* x = qkv + base + part * C;
+      const T* d = dout + base + part * C;
+      T* dx = dqkv + base + part * C;
+      float n = 0.f;
+      for (int e = 0; e < hd; ++e) { const float a = ldf<T>(x + e); n += a * a; }
+      n = sqrtf(n);
+      const float inv = 1.f / fmaxf(n, 1e-12f);
+      const float s = part == 0 ? scale[h] : 1.f;
+      float dot = 0.f;  // xhat . dq'
+      for (int e = 0; e < hd; ++e) dot += ldf<T>(x + e) * inv * ldf<T>(d + e);
+      if (part == 0) ds = dot;
+      const bool clamped = n <= 1e-12f;
+      for (int e = 0; e < hd; ++e) {
+        const float xh = ldf<T>(x + e) * inv, g = s * ldf<T>(d + e);
+        stf<T>(dx + e, clamped ? g * inv : (g - xh * s * dot) * inv);
+      }
+    }
+    for (int e = 0; e < hd; ++e) dqkv[base + 2 * C + e] = dout[base + 2 * C + e];
+  }
+  // per-head reduction of ds: heads are interleaved along idx -> reduce through LDS by head
+  __shared__ float red[64];
+  if (threadIdx.x < 64) red[threadIdx.x] = 0.f;
+  __syncthreads();
+  if (idx < rows * heads) atomicAdd(&red[h & 63], ds);
+  __syncthreads();
+  if (threadIdx.x < heads && threadIdx.x < 64 && red[threadIdx.x] != 0.f) atomicAdd(dscale + threadIdx.x, red[threadIdx.x]);
+}
+
 }  // namespace
+
+extern "C" int dfk_cosine_qk_fwd(const void* qkv, void* out, const float* scale, int64_t rows, int heads, int hd,
+                                 int dtype, hipStream_t s) {
+  if (!qkv || !out || !scale || heads <= 0 || heads > 64) return DFK_EINVAL;
+  const long n = rows * heads;
+  if (n <= 0) return 0;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (dtype == DFK_BF16)
+    hipLaunchKernelGGL(cosine_fwd_kernel<bf16raw>, grid, dim3(256), 0, s, (const bf16raw*)qkv, (bf16raw*)out, scale,
+                       (long)rows, heads, hd);
+  else
+    hipLaunchKernelGGL(cosine_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)qkv, (float*)out, scale,
+                       (long)rows, heads, hd);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, const float* scale, float* dscale,
+                                 int64_t rows, int heads, int hd, int dtype, hipStream_t s) {
+  if (!qkv || !dout || !dqkv || !scale || !dscale || heads <= 0 || heads > 64) return DFK_EINVAL;
+  const long n = rows * heads;
+  if (n <= 0) return 0;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (dtype == DFK_BF16)
+    hipLaunchKernelGGL(cosine_bwd_kernel<bf16raw>, grid, dim3(256), 0, s, (const bf16raw*)qkv, (const bf16raw*)dout,
+                       (bf16raw*)dqkv, scale, dscale, (long)rows, heads, hd);
+  else
+    hipLaunchKernelGGL(cosine_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)qkv, (const float*)dout,
+                       (float*)dqkv, scale, dscale, (long)rows, heads, hd);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int dfk_patch_im2col(const void* x, int x_dtype, void* out, int out_dtype, const dfk_im2col_args* a,
                                 hipStream_t s) {

@@ -312,6 +312,31 @@ class PosConvFn(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class CosineQKFn(torch.autograd.Function):
+    """SwinV2 cosine attention prologue: [rows, 3C] -> (normalize(q)*scale[h], normalize(k), v)."""
+
+    @staticmethod
+    def forward(ctx, qkv, scale, heads, hd):
+        out = torch.empty_like(qkv)
+        s = scale.detach().float().contiguous()
+        K.L.check(K.L.lib().dfk_cosine_qk_fwd(K.L.ptr(qkv), K.L.ptr(out), K.L.ptr(s), qkv.shape[0], heads, hd,
+                                              K.L.dt(qkv), K.L.stream()), "cosine_qk_fwd")
+        ctx.save_for_backward(qkv, s)
+        ctx.hd = hd
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, s = ctx.saved_tensors
+        heads = s.numel()
+        dqkv = torch.empty_like(qkv)
+        ds = torch.zeros(heads, device=qkv.device)
+        K.L.check(K.L.lib().dfk_cosine_qk_bwd(K.L.ptr(qkv), K.L.ptr(dout.contiguous()), K.L.ptr(dqkv), K.L.ptr(s),
+                                              K.L.ptr(ds), qkv.shape[0], heads, ctx.hd, K.L.dt(qkv), K.L.stream()),
+                  "cosine_qk_bwd")
+        return dqkv, ds, None, None
+
+
 class PatchEmbedFn(torch.autograd.Function):
     """Conv with kernel == stride as im2col + GEMM (+bias): PatchEmbed3D.proj
     (video_swin_transformer.py:436,453) / SwinV2 PatchEmbed.proj.  Returns

@@ -1,0 +1,58 @@
+"""Builders for the north-star fused model: video slot
+SwinTransformer3D (+ mean pooling, VSTFeat), mel slot SwinTransformerV2
+(use_feat), waveform slot Audio2D(wav2vec2), FusionModel head.
+
+CONFIGS mirror BASELINE.json: C1 = tiny VST 2,2,2,2 / window 4x7x7 + reduced
+mel SwinV2 + 2-layer wav2vec2 (8x112x112, 1 s); C2 = Swin-T 2,2,6,2 / window
+8x7x7 + SwinV2 (128; 2,2,18,2) + wav2vec2-base (32x224x224, 4 s); C4 =
+Swin-B video; C5 = 64 frames + 10 s audio.
+"""
+import os
+import types
+
+import torch
+
+from . import set_compute_dtype
+from .audioTransformer import Audio2D
+from .ModalFusion import FusionModel
+from .swin_transformer2d import SwinTransformerV2
+from .video_swin_transformer import SwinTransformer3D, VSTFeat
+from .wav2vec2 import Wav2Vec2Config, Wav2Vec2Model
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+W2V_CONFIG = os.path.join(HERE, "w2v_base_config.json")
+
+_VST_T = dict(patch_size=(2, 4, 4), embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24],
+              window_size=(8, 7, 7), drop_path_rate=0.0, patch_norm=True)
+_VST_B = dict(patch_size=(2, 4, 4), embed_dim=128, depths=[2, 2, 18, 2], num_heads=[4, 8, 16, 32],
+              window_size=(8, 7, 7), drop_path_rate=0.0, patch_norm=True)
+_MEL_C2 = dict(num_classes=1, use_feat=True, embed_dim=128, depths=[2, 2, 18, 2], num_heads=[4, 8, 16, 32],
+               window_size=7, drop_path_rate=0.0, pretrained_window_sizes=(16, 16, 16, 16))
+
+CONFIGS = {
+    "c1": dict(vst=dict(patch_size=(2, 4, 4), embed_dim=96, depths=[2, 2, 2, 2], num_heads=[3, 6, 12, 24],
+                        window_size=(4, 7, 7), drop_path_rate=0.0, patch_norm=True),
+               mel=dict(num_classes=1, use_feat=True, img_size=224, embed_dim=32, depths=[2, 2, 2, 2],
+                        num_heads=[1, 2, 4, 8], window_size=7, drop_path_rate=0.0,
+                        pretrained_window_sizes=(16, 16, 16, 16)),
+               w2v_layers=2, video_dim=768, audio_dim=256, T=8, H=112, W=112, seconds=1, B=2),
+    "c2": dict(vst=_VST_T, mel=_MEL_C2, w2v_layers=12, video_dim=768, audio_dim=1024, T=32, H=224, W=224,
+               seconds=4, B=8),
+    "c4": dict(vst=_VST_B, mel=_MEL_C2, w2v_layers=12, video_dim=1024, audio_dim=1024, T=32, H=224, W=224,
+               seconds=4, B=8),
+    "c5": dict(vst=_VST_T, mel=_MEL_C2, w2v_layers=12, video_dim=768, audio_dim=1024, T=64, H=224, W=224,
+               seconds=10, B=8),
+}
+
+
+def build_fused(cfg, args=None, w2v_config=W2V_CONFIG, compute_dtype=torch.float32):
+    if isinstance(cfg, str):
+        cfg = CONFIGS[cfg]
+    args = args or types.SimpleNamespace(soft=0.01, classify_drop=0.0, swin_drop=0.0)
+    vst = SwinTransformer3D(**cfg["vst"])
+    mel = SwinTransformerV2(**cfg["mel"])
+    wcfg = Wav2Vec2Config.from_json_file(w2v_config, num_hidden_layers=cfg["w2v_layers"]).deterministic()
+    pa = Audio2D(args, Wav2Vec2Model(wcfg), num_classes=1, use_feat=True)
+    m = FusionModel(args, VSTFeat(vst), mel, pa, out_dim=1, video_dim=cfg["video_dim"], audio_dim=cfg["audio_dim"],
+                    paudio_dim=768)
+    return set_compute_dtype(m, compute_dtype)

@@ -176,6 +176,15 @@ int dfk_w2v_conv0_bwd(const float* wave, int64_t B, int64_t S, const float* w, c
                       const float* beta, float eps, const float* stats, const void* dout, int dtype,
                       float* scratch, float* dw, float* dgamma, float* dbeta, hipStream_t stream);
 
+/* SwinV2 cosine-attention prologue (swin_transformer2d.py:154-157) on a [rows, 3C]
+ * qkv buffer: q' = normalize(q)*scale[h], k' = normalize(k), v' = v, so the window
+ * attention kernel then runs with scale 1 (scale = exp(clamp(logit_scale))).
+ * The backward writes dqkv and accumulates dscale[h] (fp32 +=). */
+int dfk_cosine_qk_fwd(const void* qkv, void* out, const float* scale, int64_t rows, int heads, int hd, int dtype,
+                      hipStream_t stream);
+int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, const float* scale, float* dscale,
+                      int64_t rows, int heads, int hd, int dtype, hipStream_t stream);
+
 /* dx = dy * gelu'(pre) (exact-erf GELU backward, torch nn.GELU / HF ACT2FN["gelu"]). */
 int dfk_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, int dtype, hipStream_t stream);
 

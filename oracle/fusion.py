@@ -55,6 +55,6 @@ def build_fused(cfg, w2v_config_json):
     """The fused model of tests/golden/golden_cases.py FUSED_C1-style configs."""
     vst = V.SwinTransformer3D(**cfg["vst"])
     mel = S2.SwinTransformerV2(**cfg["mel"])
-    c = W.W2VConfig(w2v_config_json, num_hidden_layers=cfg["w2v_layers"])
+    c = W.W2VConfig(w2v_config_json, num_hidden_layers=cfg["w2v_layers"], mask_time_prob=0.0)
     pa = W.Audio2D(W.Wav2Vec2Model(c))
     return FusionModel(V.VSTFeat(vst), mel, pa, out_dim=1, video_dim=cfg["video_dim"], audio_dim=cfg["audio_dim"])
