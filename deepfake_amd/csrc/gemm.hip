@@ -1,12 +1,17 @@
-// Generic MFMA GEMM for gfx950 with operand views (plain / transposed /
-// implicit-conv), batching, split-K and fused epilogues.  See include/dfk.h.
+// Generic MFMA GEMM for gfx950 with operand views (plain / k-major / implicit
+// conv), batching, split-K and fused epilogues.  See include/dfk.h.
 //
 // Tile 128x128 per 256-thread workgroup (4 waves, 2x2, 64x64 each).
 //   bf16: v_mfma_f32_16x16x32_bf16, BK = 64 (2 MFMA k-steps per staged tile)
 //   f32 : v_mfma_f32_16x16x4_f32   (exact fp32, parity mode), BK = 32
-// Staging: global -> registers (16-B vectors along the contiguous dim of each
-// view) -> LDS tile stored [row][k] (k contiguous); the next tile's global
-// loads are issued before the current tile's MFMAs (register prefetch).
+// Staging: global -> registers (16-B vectors along each view's contiguous dim)
+// -> LDS in the view's NATURAL orientation:
+//   k-contiguous operand  -> tile [row][k]  : fragments by ds_read_b128
+//   k-major operand       -> tile [k][row]  : bf16 fragments by two
+//                            ds_read_b64_tr_b16 (hardware transpose), so the
+//                            dX / dW GEMMs of every Linear never scatter.
+// LDS is double-buffered: the next tile's global loads are in flight during
+// the current tile's MFMAs, one barrier per k-tile.
 #include "common.h"
 
 namespace {
@@ -14,98 +19,151 @@ namespace {
 constexpr int BM = 128, BN = 128, NT = 256;
 
 template <typename T> struct GT;
-template <> struct GT<bf16raw> { static constexpr int BK = 64, VEC = 8, PAD = 8; };
-template <> struct GT<float> { static constexpr int BK = 32, VEC = 4, PAD = 4; };
+template <> struct GT<bf16raw> { static constexpr int BK = 64, VEC = 8, PADR = 8, PADK = 16; };
+template <> struct GT<float> { static constexpr int BK = 32, VEC = 4, PADR = 4, PADK = 4; };
+
+// LDS tile geometry for one operand (ROWS x BK): [row][k] or [k][row]
+template <typename T, bool KMAJ, int ROWS>
+struct Tile {
+  static constexpr int TBK = GT<T>::BK;
+  static constexpr int STRIDE = KMAJ ? ROWS + GT<T>::PADK : TBK + GT<T>::PADR;   // elements
+  static constexpr int ELEMS = KMAJ ? TBK * STRIDE : ROWS * STRIDE;
+};
 
 // element offset of V(r, c), or -1 when it lies in the conv view's zero padding
+template <bool CONV>
 __device__ __forceinline__ long view_off(const dfk_view& v, long r, long c) {
-  if (v.conv_cg > 0) {
-    const long kk = c / v.conv_cg;
-    const long row = r * v.conv_stride + kk - v.conv_pad;
-    if (row < 0 || row >= v.conv_rows) return -1;
-    return row * v.ld + (c - kk * v.conv_cg);
+  if constexpr (CONV) {
+    if (v.conv_cg > 0) {
+      const long kk = c / v.conv_cg;
+      const long row = r * v.conv_stride + kk - v.conv_pad;
+      if (row < 0 || row >= v.conv_rows) return -1;
+      return row * v.ld + (c - kk * v.conv_cg);
+    }
   }
   return r * v.ld + c;
 }
 
-// 16-byte load of VEC contiguous elements V(r, c .. c+VEC-1); zero outside the
-// view (rok false, c >= climit, conv padding).  `vec` (host-checked alignment of
-// ptr/ld/batch strides/conv group) selects the vector load; otherwise (odd
-// shapes such as the out_dim=1 classifier) element-wise loads.
-template <typename T>
-__device__ __forceinline__ uint4 view_load(const T* base, const dfk_view& v, long r, long c, bool rok, long climit,
-                                           bool vec) {
+// VEC contiguous elements V(r, c..c+VEC-1); zeros outside the view.
+// VECOK: host guarantees 16-B alignment and whole-vector extents -> one vector load.
+// Otherwise elements are assembled in registers (odd shapes, e.g. out_dim=1).
+template <typename T, bool VECOK, bool CONV>
+__device__ __forceinline__ uint4 view_load(const T* base, const dfk_view& v, long r, long c, bool rok, long climit) {
   constexpr int VEC = 16 / sizeof(T);
   uint4 z = make_uint4(0, 0, 0, 0);
   if (!rok || c >= climit) return z;
-  if (vec && c + VEC <= climit) {
-    const long o = view_off(v, r, c);
+  if constexpr (VECOK) {
+    const long o = view_off<CONV>(v, r, c);
     return o < 0 ? z : *reinterpret_cast<const uint4*>(base + o);
-  }
-  T* e = reinterpret_cast<T*>(&z);
+  } else {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    if (c + i < climit) {
-      const long o = view_off(v, r, c + i);
-      if (o >= 0) e[i] = base[o];
+    for (int i = 0; i < VEC; ++i) {
+      if (c + i < climit) {
+        const long o = view_off<CONV>(v, r, c + i);
+        if (o >= 0) {
+          if constexpr (sizeof(T) == 2) {
+            w[i >> 1] |= (uint32_t)(*reinterpret_cast<const uint16_t*>(base + o)) << (16 * (i & 1));
+          } else {
+            w[i] = *reinterpret_cast<const uint32_t*>(base + o);
+          }
+        }
+      }
     }
+    return make_uint4(w[0], w[1], w[2], w[3]);
   }
-  return z;
 }
 
-template <typename T>
-__device__ __forceinline__ void scatter_col(T* lds, int stride, int r0, int kcol, uint4 val) {
-  // write VEC elements (consecutive rows r0.., fixed k column) — transposed staging
-  const T* e = reinterpret_cast<const T*>(&val);
-#pragma unroll
-  for (int i = 0; i < GT<T>::VEC; ++i) lds[(r0 + i) * stride + kcol] = e[i];
-}
-
-template <typename T, bool KMAJ, int ROWS>
+// stage one ROWS x BK operand tile: global -> 4 x 16-B registers per thread
+template <typename T, bool KMAJ, int ROWS, bool VECOK, bool CONV>
 __device__ __forceinline__ void load_tile(const T* base, const dfk_view& v, int row0, int rowlim, int k0, int klim,
-                                          int tid, bool vec, uint4 (&r)[4]) {
+                                          int tid, uint4 (&r)[4]) {
   constexpr int TBK = GT<T>::BK, VEC = GT<T>::VEC;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int idx = tid + s * NT;
-    if (!KMAJ) {  // view rows = tile rows, contiguous along k
+    if constexpr (!KMAJ) {   // view rows = tile rows, contiguous along k
       const int i = idx / (TBK / VEC), kc = idx % (TBK / VEC);
       const int gr = row0 + i, gk = k0 + kc * VEC;
-      r[s] = view_load<T>(base, v, gr, gk, gr < rowlim, klim, vec);
-    } else {      // view rows = k, contiguous along tile rows
+      r[s] = view_load<T, VECOK, CONV>(base, v, gr, gk, gr < rowlim, klim);
+    } else {                 // view rows = k, contiguous along tile rows
       const int k = idx / (ROWS / VEC), ic = idx % (ROWS / VEC);
       const int gk = k0 + k, gr = row0 + ic * VEC;
-      r[s] = view_load<T>(base, v, gk, gr, gk < klim, rowlim, vec);
+      r[s] = view_load<T, VECOK, CONV>(base, v, gk, gr, gk < klim, rowlim);
     }
   }
 }
 
 template <typename T, bool KMAJ, int ROWS>
 __device__ __forceinline__ void store_tile(T* lds, int tid, const uint4 (&r)[4]) {
-  constexpr int TBK = GT<T>::BK, VEC = GT<T>::VEC, S = TBK + GT<T>::PAD;
+  using TL = Tile<T, KMAJ, ROWS>;
+  constexpr int TBK = GT<T>::BK, VEC = GT<T>::VEC;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int idx = tid + s * NT;
-    if (!KMAJ) {
+    if constexpr (!KMAJ) {
       const int i = idx / (TBK / VEC), kc = idx % (TBK / VEC);
-      *reinterpret_cast<uint4*>(lds + i * S + kc * VEC) = r[s];
+      *reinterpret_cast<uint4*>(lds + i * TL::STRIDE + kc * VEC) = r[s];
     } else {
       const int k = idx / (ROWS / VEC), ic = idx % (ROWS / VEC);
-      scatter_col<T>(lds, S, ic * VEC, k, r[s]);
+      *reinterpret_cast<uint4*>(lds + k * TL::STRIDE + ic * VEC) = r[s];
     }
   }
 }
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v lds_short4;
 
-template <typename T, bool AK, bool BK>
-__global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int avec, int bvec) {
-  constexpr int TBK = GT<T>::BK, S = TBK + GT<T>::PAD;
-  __shared__ __attribute__((aligned(16))) T As[BM * S];
-  __shared__ __attribute__((aligned(16))) T Bs[BN * S];
+// bf16 MFMA fragment: 8 consecutive k (kb..kb+7) of tile row r (lane&15 within a 16-row block)
+template <bool KMAJ, int ROWS>
+__device__ __forceinline__ bf16x8 frag_bf16(const bf16raw* lds, int r0, int kb, int lane) {
+  using TL = Tile<bf16raw, KMAJ, ROWS>;
+  if constexpr (!KMAJ) {
+    return *reinterpret_cast<const bf16x8*>(lds + (r0 + (lane & 15)) * TL::STRIDE + kb + (lane >> 4) * 8);
+  } else {
+    // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row (k) q, columns 4p..4p+3;
+    // lane i of the group receives column i of the 4 rows.
+    const int li = lane & 15, q = li >> 2, p = li & 3;
+    const int k = kb + (lane >> 4) * 8 + q;
+    const bf16raw* a0 = lds + k * TL::STRIDE + r0 + 4 * p;
+    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(a0));
+    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(a0 + 4 * TL::STRIDE));
+    short8 u = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, u);
+  }
+}
+
+// fp32 MFMA (16x16x4) operand: element [row r0+(lane&15)][k = kb + (lane>>4)]
+template <bool KMAJ, int ROWS>
+__device__ __forceinline__ float frag_f32(const float* lds, int r0, int kb, int lane) {
+  using TL = Tile<float, KMAJ, ROWS>;
+  if constexpr (!KMAJ) return lds[(r0 + (lane & 15)) * TL::STRIDE + kb + (lane >> 4)];
+  else return lds[(kb + (lane >> 4)) * TL::STRIDE + r0 + (lane & 15)];
+}
+
+template <typename T, bool AK, bool BKM, bool VECOK, bool CONV>
+__global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int evec) {
+  using TA = Tile<T, AK, BM>;
+  using TB = Tile<T, BKM, BN>;
+  constexpr int TBK = GT<T>::BK;
+  constexpr int BUF = TA::ELEMS + TB::ELEMS;
+  constexpr int ES = 64 + 4;                      // epilogue staging row stride (fp32)
+  constexpr int SMEM_T = 2 * BUF > (4 * 64 * ES * 4) / (int)sizeof(T) ? 2 * BUF : (4 * 64 * ES * 4) / (int)sizeof(T);
+  __shared__ __attribute__((aligned(16))) T smem[SMEM_T];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int bn = blockIdx.x * BN, bm = blockIdx.y * BM;
+  // XCD-aware tile order (blocks b and b+8 share an XCD's L2): consecutive remapped ids —
+  // the N-tiles of one M-panel — land on one XCD and re-read A from its L2.
+  int tn, tmi;
+  {
+    const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    const int nid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    tn = nid % gridDim.x;
+    tmi = nid / gridDim.x;
+  }
+  const int bn = tn * BN, bm = tmi * BM;
   int z = blockIdx.z;
   const int split = z % g.splitk;
   z /= g.splitk;
@@ -123,29 +181,29 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
 
   uint4 ra[4], rb[4];
   if (kbeg < kend) {
-    load_tile<T, AK, BM>(A, g.a, bm, g.M, kbeg, kend, tid, avec, ra);
-    load_tile<T, BK, BN>(B, g.b, bn, g.N, kbeg, kend, tid, bvec, rb);
-    store_tile<T, AK, BM>(As, tid, ra);
-    store_tile<T, BK, BN>(Bs, tid, rb);
+    load_tile<T, AK, BM, VECOK, CONV>(A, g.a, bm, g.M, kbeg, kend, tid, ra);
+    load_tile<T, BKM, BN, VECOK, CONV>(B, g.b, bn, g.N, kbeg, kend, tid, rb);
+    store_tile<T, AK, BM>(smem, tid, ra);
+    store_tile<T, BKM, BN>(smem + TA::ELEMS, tid, rb);
   }
   __syncthreads();
+  int cur = 0;
   for (int k0 = kbeg; k0 < kend; k0 += TBK) {
     const bool more = k0 + TBK < kend;
     if (more) {
-      load_tile<T, AK, BM>(A, g.a, bm, g.M, k0 + TBK, kend, tid, avec, ra);
-      load_tile<T, BK, BN>(B, g.b, bn, g.N, k0 + TBK, kend, tid, bvec, rb);
+      load_tile<T, AK, BM, VECOK, CONV>(A, g.a, bm, g.M, k0 + TBK, kend, tid, ra);
+      load_tile<T, BKM, BN, VECOK, CONV>(B, g.b, bn, g.N, k0 + TBK, kend, tid, rb);
     }
+    const T* As = smem + cur * BUF;
+    const T* Bs = As + TA::ELEMS;
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int ks = 0; ks < TBK / 32; ++ks) {
         bf16x8 af[4], bfr[4];
-        const int kof = ks * 32 + (lane >> 4) * 8;
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-          af[mi] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + mi * 16 + (lane & 15)) * S + kof);
+        for (int mi = 0; mi < 4; ++mi) af[mi] = frag_bf16<AK, BM>(As, wm * 64 + mi * 16, ks * 32, lane);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          bfr[ni] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + ni * 16 + (lane & 15)) * S + kof);
+        for (int ni = 0; ni < 4; ++ni) bfr[ni] = frag_bf16<BKM, BN>(Bs, wn * 64 + ni * 16, ks * 32, lane);
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -156,11 +214,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
 #pragma unroll
       for (int ks = 0; ks < TBK / 4; ++ks) {
         float af[4], bfr[4];
-        const int kof = ks * 4 + (lane >> 4);
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) af[mi] = As[(wm * 64 + mi * 16 + (lane & 15)) * S + kof];
+        for (int mi = 0; mi < 4; ++mi) af[mi] = frag_f32<AK, BM>(As, wm * 64 + mi * 16, ks * 4, lane);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) bfr[ni] = Bs[(wn * 64 + ni * 16 + (lane & 15)) * S + kof];
+        for (int ni = 0; ni < 4; ++ni) bfr[ni] = frag_f32<BKM, BN>(Bs, wn * 64 + ni * 16, ks * 4, lane);
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -168,49 +225,92 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
       }
     }
-    __syncthreads();
     if (more) {
-      store_tile<T, AK, BM>(As, tid, ra);
-      store_tile<T, BK, BN>(Bs, tid, rb);
-      __syncthreads();
+      store_tile<T, AK, BM>(smem + (cur ^ 1) * BUF, tid, ra);
+      store_tile<T, BKM, BN>(smem + (cur ^ 1) * BUF + TA::ELEMS, tid, rb);
     }
+    __syncthreads();
+    cur ^= 1;
   }
 
-  // ---- epilogue
+  // ---- epilogue: stage each wave's 64x64 fp32 tile through LDS (the 16x16 MFMA C/D
+  // layout is col = lane&15, row = (lane>>4)*4 + r), then every lane owns 8
+  // consecutive columns of a row: 16-B loads of bias/residual/aux and 16-B stores.
+  float* es = reinterpret_cast<float*>(smem) + wave * 64 * ES;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) es[(mi * 16 + (lane >> 4) * 4 + r) * ES + ni * 16 + (lane & 15)] = acc[mi][ni][r];
+  __syncthreads();
   const T* bias = g.bias ? reinterpret_cast<const T*>(g.bias) + z1 * g.bias_bs1 : nullptr;
   const T* res = g.residual ? reinterpret_cast<const T*>(g.residual) + z0 * g.rbs0 + z1 * g.rbs1 : nullptr;
   const long coff = z0 * g.cbs0 + z1 * g.cbs1;
   T* aux = g.aux ? reinterpret_cast<T*>(g.aux) + coff : nullptr;
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int col = bn + wn * 64 + ni * 16 + (lane & 15);
-      if (col >= g.N) continue;
-      const float bv = bias ? ldf<T>(bias + col) : 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = bm + wm * 64 + mi * 16 + (lane >> 4) * 4 + r;
-        if (row >= g.M) continue;
-        float v = acc[mi][ni][r] + bv;
-        if (g.act == 1) {
-          if (aux) stf<T>(aux + (long)row * g.ldaux + col, v);
-          v = gelu_f(v);
-        } else if (g.act == 2) {
-          v *= dgelu_f(ldf<T>(aux + (long)row * g.ldaux + col));
-        }
-        if (res) v += ldf<T>(res + (long)row * g.ldr + col);
-        const long ci = coff + (long)row * g.ldc + col;
-        if (g.atomic) {
-          atomicAdd(reinterpret_cast<float*>(g.c) + ci, v);
-        } else if (g.c_f32) {
-          float* C = reinterpret_cast<float*>(g.c) + ci;
-          *C = g.beta != 0.f ? v + g.beta * *C : v;
-        } else {
-          T* C = reinterpret_cast<T*>(g.c) + ci;
-          stf<T>(C, g.beta != 0.f ? v + g.beta * ldf<T>(C) : v);
-        }
+  if (g.atomic || g.c_f32) {
+    // fp32 output (weight gradients): one row per wave instruction = 256 contiguous bytes
+    const int col = bn + wn * 64 + lane;
+    float* Cb = reinterpret_cast<float*>(g.c) + coff;
+#pragma unroll 4
+    for (int rl = 0; rl < 64; ++rl) {
+      const int row = bm + wm * 64 + rl;
+      if (row >= g.M || col >= g.N) continue;
+      float v = es[rl * ES + lane];
+      if (bias) v += ldf<T>(bias + col);
+      if (res) v += ldf<T>(res + (long)row * g.ldr + col);
+      float* C = Cb + (long)row * g.ldc + col;
+      if (g.atomic) atomicAdd(C, v);
+      else *C = g.beta != 0.f ? v + g.beta * *C : v;
+    }
+    return;
+  }
+  const int c8 = (lane & 7) * 8;
+  const int col0 = bn + wn * 64 + c8;
+#pragma unroll 1
+  for (int pass = 0; pass < 8; ++pass) {
+    const int rl = pass * 8 + (lane >> 3);
+    const int row = bm + wm * 64 + rl;
+    if (row >= g.M || col0 >= g.N) continue;
+    float v[8];
+    *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(es + rl * ES + c8);
+    *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(es + rl * ES + c8 + 4);
+    const bool full = evec && col0 + 8 <= g.N;
+    const int ncol = min(8, g.N - col0);
+    if (bias) {
+      if (full) { float b8[8]; ld8<T>(bias + col0, b8); for (int e = 0; e < 8; ++e) v[e] += b8[e]; }
+      else for (int e = 0; e < ncol; ++e) v[e] += ldf<T>(bias + col0 + e);
+    }
+    if (g.act == 1) {
+      T* ap = aux ? aux + (long)row * g.ldaux + col0 : nullptr;
+      if (ap) { if (full) st8<T>(ap, v); else for (int e = 0; e < ncol; ++e) stf<T>(ap + e, v[e]); }
+      for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+    } else if (g.act == 2) {
+      const T* ap = aux + (long)row * g.ldaux + col0;
+      float a8[8];
+      if (full) ld8<T>(ap, a8); else for (int e = 0; e < ncol; ++e) a8[e] = ldf<T>(ap + e);
+      for (int e = 0; e < 8; ++e) v[e] *= dgelu_f(a8[e]);
+    }
+    if (res) {
+      const T* rp = res + (long)row * g.ldr + col0;
+      if (full) { float r8[8]; ld8<T>(rp, r8); for (int e = 0; e < 8; ++e) v[e] += r8[e]; }
+      else for (int e = 0; e < ncol; ++e) v[e] += ldf<T>(rp + e);
+    }
+    const long ci = coff + (long)row * g.ldc + col0;
+    if (g.atomic) {
+      float* C = reinterpret_cast<float*>(g.c) + ci;
+      for (int e = 0; e < ncol; ++e) atomicAdd(C + e, v[e]);
+    } else if (g.c_f32) {
+      float* C = reinterpret_cast<float*>(g.c) + ci;
+      for (int e = 0; e < ncol; ++e) C[e] = g.beta != 0.f ? v[e] + g.beta * C[e] : v[e];
+    } else {
+      T* C = reinterpret_cast<T*>(g.c) + ci;
+      if (g.beta != 0.f) {
+        if (full) { float c8v[8]; ld8<T>(C, c8v); for (int e = 0; e < 8; ++e) v[e] += g.beta * c8v[e]; }
+        else for (int e = 0; e < ncol; ++e) v[e] += g.beta * ldf<T>(C + e);
       }
+      if (full) st8<T>(C, v);
+      else for (int e = 0; e < ncol; ++e) stf<T>(C + e, v[e]);
     }
   }
 }
@@ -225,7 +325,7 @@ __global__ void colsum_kernel(const T* __restrict__ x, long rows, int cols, long
   atomicAdd(out + j, s);
 }
 
-// 16-byte vector loads are legal for this view (else the element-wise path runs)
+// 16-byte vector loads are legal for this view (else the element-wise instantiation runs)
 bool view_vec(const dfk_view& v, int vec) {
   if (v.ld % vec || v.bs0 % vec || v.bs1 % vec) return false;
   if ((reinterpret_cast<uintptr_t>(v.ptr) & 15) != 0) return false;
@@ -233,12 +333,24 @@ bool view_vec(const dfk_view& v, int vec) {
   return true;
 }
 
+template <typename T, bool VECOK, bool CONV>
+void dispatch(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, hipStream_t s) {
+  if (g.a_kmajor) {
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, true, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec);
+    else hipLaunchKernelGGL((gemm_kernel<T, true, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec);
+  } else {
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, false, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec);
+    else hipLaunchKernelGGL((gemm_kernel<T, false, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec);
+  }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 template <typename T>
 int launch(const dfk_gemm_args& g, hipStream_t s) {
   constexpr int VEC = GT<T>::VEC, TBK = GT<T>::BK;
   if (!g.a.ptr || !g.b.ptr || !g.c) return DFK_EINVAL;
   if ((g.a.conv_cg > 0 && g.a.conv_stride <= 0) || (g.b.conv_cg > 0 && g.b.conv_stride <= 0)) return DFK_EINVAL;
-  const int avec = view_vec(g.a, VEC), bvec = view_vec(g.b, VEC);
   if (g.splitk < 1 || g.nz0 < 1 || g.nz1 < 1) return DFK_EINVAL;
   if (g.splitk > 1 && !g.atomic) return DFK_EINVAL;
   if (g.atomic && (!g.c_f32 || g.bias || g.residual || g.act)) return DFK_EINVAL;
@@ -248,12 +360,20 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   kchunk = dfk_cdiv(kchunk, TBK) * TBK;
   dim3 grid(dfk_cdiv(g.N, BN), dfk_cdiv(g.M, BM), g.nz0 * g.nz1 * g.splitk);
   if (grid.y > 65535 || grid.z > 65535) return DFK_EINVAL;
-  if (g.a_kmajor) {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, true, true>), grid, dim3(NT), 0, s, g, kchunk, avec, bvec);
-    else hipLaunchKernelGGL((gemm_kernel<T, true, false>), grid, dim3(NT), 0, s, g, kchunk, avec, bvec);
+  // vector path also needs the contiguous extents to be whole vectors (else tails load element-wise)
+  const bool vec = view_vec(g.a, VEC) && view_vec(g.b, VEC) && (g.a_kmajor ? g.M : g.K) % VEC == 0 &&
+                   (g.b_kmajor ? g.N : g.K) % VEC == 0;
+  // epilogue 16-B path: 8-element groups of C / residual / aux / bias rows stay 16-B aligned
+  const bool evec = !g.c_f32 && aligned16(g.c) && g.ldc % 8 == 0 && g.cbs0 % 8 == 0 && g.cbs1 % 8 == 0 &&
+                    (!g.bias || (aligned16(g.bias) && g.bias_bs1 % 8 == 0)) &&
+                    (!g.residual || (aligned16(g.residual) && g.ldr % 8 == 0 && g.rbs0 % 8 == 0 && g.rbs1 % 8 == 0)) &&
+                    (!g.aux || (aligned16(g.aux) && g.ldaux % 8 == 0));
+  const bool conv = g.a.conv_cg > 0 || g.b.conv_cg > 0;
+  if (vec) {
+    if (conv) dispatch<T, true, true>(g, grid, kchunk, evec, s);
+    else dispatch<T, true, false>(g, grid, kchunk, evec, s);
   } else {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, false, true>), grid, dim3(NT), 0, s, g, kchunk, avec, bvec);
-    else hipLaunchKernelGGL((gemm_kernel<T, false, false>), grid, dim3(NT), 0, s, g, kchunk, avec, bvec);
+    dispatch<T, false, true>(g, grid, kchunk, evec, s);
   }
   DFK_CHECK_LAUNCH();
   return 0;

@@ -307,7 +307,11 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
 #define LAUNCH_F(T, HD)                                                                                 \
   do {                                                                                                  \
     auto kfn = wattn_fwd_kernel<T, HD>;                                                                 \
-    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    static bool attr_set = false;  /* once per kernel: the 160 KiB LDS limit (never inside a capture) */ \
+    if (!attr_set) {                                                                                    \
+      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      attr_set = true;                                                                                  \
+    }                                                                                                   \
     hipLaunchKernelGGL(kfn, grid, dim3(256), lds, s, a, g, qsplit);                                     \
   } while (0)
   if (a.dtype == DFK_BF16) {
@@ -626,7 +630,11 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
 #define LAUNCH_B(T, HD)                                                                                 \
   do {                                                                                                  \
     auto kfn = wattn_bwd_kernel<T, HD>;                                                                 \
-    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    static bool attr_set = false;  /* once per kernel: the 160 KiB LDS limit (never inside a capture) */ \
+    if (!attr_set) {                                                                                    \
+      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      attr_set = true;                                                                                  \
+    }                                                                                                   \
     for (int q0 = 0; q0 < g.Np; q0 += Qn)                                                               \
       hipLaunchKernelGGL(kfn, grid, dim3(256), lds, s, *bp, g, q0, std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0); \
   } while (0)

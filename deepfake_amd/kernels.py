@@ -10,7 +10,7 @@ import torch
 
 from . import _lib as L
 
-_CU_TARGET_BLOCKS = 2048  # split-K target grid for skinny weight-gradient GEMMs
+_CU_TARGET_BLOCKS = 512  # split-K target grid for skinny weight-gradient GEMMs (2 per CU; fewer atomics)
 
 
 def _view(t, ld, bs0=0, bs1=0, conv=None):

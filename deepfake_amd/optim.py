@@ -1,0 +1,55 @@
+"""Fused SGD + CosineAnnealingLR over a ParamStore (src/trainer.py:80-85,295-297).
+
+torch.optim.SGD(lr, momentum=0.9, weight_decay=wd) semantics (dampening 0,
+no nesterov; first step buf = g) in one HBM-bound kernel over the flat fp32
+buffer, which also rewrites the bf16 compute shadow.  The learning rate lives
+in device memory so a captured graph replays with the scheduler's current lr.
+"""
+import math
+
+import torch
+
+from . import kernels as K
+
+
+class FusedSGD:
+    def __init__(self, store, lr, momentum=0.9, weight_decay=0.0):
+        self.store = store
+        self.base_lr = float(lr)
+        self.momentum, self.weight_decay = float(momentum), float(weight_decay)
+        self.buf = torch.zeros_like(store.flat)
+        self.lr_dev = torch.full((1,), self.base_lr, device=store.flat.device, dtype=torch.float32)
+        self.param_groups = [{"lr": self.base_lr, "initial_lr": self.base_lr}]
+        self.first = True
+
+    def set_lr(self, lr):
+        self.param_groups[0]["lr"] = float(lr)
+        self.lr_dev.fill_(float(lr))
+
+    def step(self, first=None):
+        f = self.first if first is None else first
+        K.sgd_step(self.store.flat, self.store.grad, self.buf, self.store.shadow, 0.0, self.momentum,
+                   self.weight_decay, f, lr_dev=self.lr_dev)
+        self.first = False
+
+    def zero_grad(self):
+        self.store.zero_grad()
+
+    def state_dict(self):
+        return {"momentum_buffer": self.buf, "lr": self.param_groups[0]["lr"], "first": self.first}
+
+
+class CosineAnnealingLR:
+    """torch.optim.lr_scheduler.CosineAnnealingLR (eta_min 0) closed form, stepped per optimizer step."""
+
+    def __init__(self, optimizer, T_max, eta_min=0.0):
+        self.opt, self.T_max, self.eta_min = optimizer, max(int(T_max), 1), eta_min
+        self.t = 0
+
+    def get_lr(self):
+        base = self.opt.base_lr
+        return self.eta_min + (base - self.eta_min) * (1 + math.cos(math.pi * self.t / self.T_max)) / 2
+
+    def step(self):
+        self.t += 1
+        self.opt.set_lr(self.get_lr())

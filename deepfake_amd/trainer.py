@@ -1,0 +1,225 @@
+"""Trainer — the reference's src/trainer.py surface (Trainer(model, args, device,
+dataset, logger, processor), .train(), .eval(), .run_batch(), .load_ckpt())
+re-built MI355X-first:
+
+* one process per GPU (torchrun), RCCL all-reduce of flat gradient buckets
+  overlapped with backward (deepfake_amd.ddp) instead of DataParallel
+  (src/trainer.py:74-75);
+* parameters / gradients in flat buffers with a bf16 compute shadow
+  (deepfake_amd.params), fused SGD(momentum 0.9, weight decay) +
+  CosineAnnealingLR (src/trainer.py:80-85) with the lr in device memory;
+* BCELoss on the sigmoid output (src/trainer.py:88,132), accuracy
+  (prob >= 0.5) == label (:142-144), gradient accumulation over accum_step
+  micro-batches with the all-reduce only on the last one (:280-297);
+* host<->device synchronisation only at log steps (the reference syncs every
+  step at :133,136);
+* optional HIP-graph capture of the whole step (TrainStep(graph=True)).
+"""
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from .ddp import GradBucketer
+from .optim import CosineAnnealingLR, FusedSGD
+from .params import ParamStore
+from .utils import AverageMeter, Logger
+
+
+def normalize_wave(w):
+    """Wav2Vec2FeatureExtractor zero-mean / unit-variance (HF feature_extraction_wav2vec2.py:94-95),
+    on device, for equal-length clips (src/trainer.py:258)."""
+    m = w.mean(-1, keepdim=True)
+    v = w.var(-1, keepdim=True, unbiased=False)
+    return (w - m) / torch.sqrt(v + 1e-7)
+
+
+class TrainStep:
+    """fwd + BCE + bwd + gradient all-reduce + SGD for one micro-batch, optionally
+    captured once into a HIP graph and replayed (inputs copied into static buffers)."""
+
+    def __init__(self, model, store, opt, bucketer, graph=False):
+        self.model, self.store, self.opt, self.bucketer = model, store, opt, bucketer
+        self.lossF = torch.nn.BCELoss()
+        self.graph_mode = graph
+        self.graph = None
+        self.static = None
+
+    def _fwd_bwd(self, feature, label):
+        prob = self.model(feature)
+        loss = self.lossF(prob.float().reshape(-1), label.float().reshape(-1))
+        loss.backward()
+        return loss, prob
+
+    def eager(self, feature, label):
+        loss, prob = self._fwd_bwd(feature, label)
+        self.bucketer.finish()          # overlapped bucket all-reduces (hooks), then average
+        self.opt.step()                 # first call initialises the momentum buffer (torch SGD semantics)
+        self.store.zero_grad()
+        # detach: a live autograd graph would pin AccumulateGrad nodes to this stream (breaks capture)
+        return loss.detach(), prob.detach()
+
+    def __call__(self, feature, label):
+        if not self.graph_mode:
+            return self.eager(feature, label)
+        if self.graph is None:
+            return self._capture(feature, label)
+        for s, x in zip(self.static[0], feature):
+            s.copy_(x, non_blocking=True)
+        self.static[1].copy_(label, non_blocking=True)
+        self.graph.replay()
+        return self.static[2], self.static[3]
+
+    def _capture(self, feature, label):
+        """One eager step (initialises momentum, allocator warm-up), then capture the
+        whole step — grad zeroing, fwd, bwd, bucket all-reduces, SGD — as one graph."""
+        loss, prob = self.eager(feature, label)
+        torch.cuda.synchronize()
+        static_in = [x.clone() for x in feature]
+        static_label = label.clone()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        self.bucketer.overlap = False
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self.store.grad.zero_()
+                l2, p2 = self._fwd_bwd(tuple(static_in), static_label)
+                self.bucketer.allreduce_all()
+                self.opt.step(first=False)
+        torch.cuda.current_stream().wait_stream(s)
+        self.bucketer.overlap = True
+        self.bucketer.reset()
+        self.graph = g
+        self.static = (static_in, static_label, l2, p2)
+        return loss, prob
+
+
+class Trainer:
+    def __init__(self, model, args, device, dataset, logger=None, processor=None, compute_dtype=None, graph=False):
+        self.train_epochs = args.epochs
+        self.device = device
+        self.lr = args.learning_rate
+        self.batch_size = args.batch_size
+        self.modality = args.modality
+        self.logger = logger or Logger(None)
+        self.processor = processor
+        self.model_save = args.model_save
+        self.log_step = args.log_step
+        self.start_epoch = 0
+        self.accum_step = max(1, int(args.accum_step))
+        self.dataset = dataset
+        self.trainloader = dataset.train_dataloader()
+        self.valloader = dataset.val_dataloader()
+        dt = compute_dtype or (torch.bfloat16 if getattr(args, "dtype", "bf16") == "bf16" else torch.float32)
+        model.to(device)
+        self.model_s = self.model = model
+        self.store = ParamStore(model, dt)
+        self.bucketer = GradBucketer(self.store, bucket_mb=getattr(args, "bucket_mb", 64.0))
+        self.bucketer.broadcast_buffers(model)
+        if self.bucketer.enabled:                      # identical replicas: parameters from rank 0
+            dist.broadcast(self.store.flat, 0)
+            self.store.refresh_shadow()
+        self.optimizer = FusedSGD(self.store, args.learning_rate, momentum=0.9, weight_decay=args.l2_decacy)
+        steps_per_epoch = max(1, int(len(self.trainloader) / self.accum_step))
+        self.scheduler = CosineAnnealingLR(self.optimizer, T_max=self.train_epochs * steps_per_epoch)
+        self.step_fn = TrainStep(model, self.store, self.optimizer, self.bucketer, graph=graph)
+        self.lossF = torch.nn.BCELoss()
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        n = sum(p.numel() for p in model.parameters())
+        self.logger(f"model params: {n / 1e6:.3f} M ({n * 4 / 2 ** 20:.1f} MiB fp32)")
+
+    def load_ckpt(self, args):
+        """src/trainer.py:90-122: {'checkpoint': state_dict} with strict=False and
+        'module.' stripping for single-modality runs; optimizer/epoch not restored."""
+        path = args.fused_ckpt_path if self.modality == "fused" else (
+            args.audio_ckpt_path if self.modality == "audio" else args.video_ckpt_path)
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        sd = ck["checkpoint"]
+        if self.modality != "fused":
+            sd = {(k[7:] if k.startswith("module.") else k): v for k, v in sd.items()}
+        self.model_s.load_state_dict(sd, strict=False)
+        self.store.refresh_shadow()
+        self.logger("Load Finetuned Model Succesfully")
+
+    def save_ckpt(self, path, epoch):
+        if self.rank == 0:
+            torch.save({"epoch": epoch, "checkpoint": self.model_s.state_dict(),
+                        "optimizer": self.optimizer.state_dict()}, path)
+
+    def _prep(self, batch):
+        feat, label = batch[0], batch[1]
+        if self.modality == "fused":
+            video, mel, wave = feat["Video"], feat["Audio"], feat["PAudio"]
+            if isinstance(wave, (list, tuple)):
+                wave = torch.stack([torch.as_tensor(w) for w in wave])
+            wave = normalize_wave(wave.to(self.device, non_blocking=True).float())
+            feature = (video.to(self.device, non_blocking=True), mel.to(self.device, non_blocking=True), wave)
+        else:
+            feature = feat.to(self.device, non_blocking=True)
+        return feature, label.to(self.device, non_blocking=True)
+
+    def run_batch(self, feature, label, gpu_log=None):
+        """Forward + loss + accuracy (src/trainer.py:124-148); no host sync here."""
+        out = self.model(feature)
+        loss = self.lossF(out.float().reshape(-1), label.float().reshape(-1))
+        with torch.no_grad():
+            acc = ((out.reshape(-1) >= 0.5) == label.reshape(-1).to(torch.bool)).float().mean()
+        return {"loss": loss, "acc": acc}
+
+    def eval(self, dataloader, epoch, t, lr, val_loss_draw=None, gpu_log=None):
+        stat = AverageMeter()
+        self.model.eval()
+        with torch.no_grad():
+            for batch in dataloader:
+                feature, label = self._prep(batch)
+                r = self.run_batch(feature, label)
+                if t % self.log_step == 0:
+                    self.logger("| epoch {:2d} | step {:4d} | lr {:.4E} | Val Loss {:3.5f} | Val Acc {:1.5f} ".format(
+                        epoch, t, lr, r["loss"].item(), r["acc"].item()))
+                stat.update(r["loss"].item())
+                t += 1
+        self.logger(f"Phase:val, Avg Loss:{stat.avg}")
+        return t
+
+    def train(self):
+        t = 0
+        stat = AverageMeter()
+        self.logger("[INFO] Start training, lr = {:.6f}".format(self.optimizer.param_groups[0]["lr"]))
+        for epoch in range(self.start_epoch, self.train_epochs + 1):
+            self.model.train()
+            self.store.zero_grad()
+            t0 = time.time()
+            for iter_id, batch in enumerate(self.trainloader):
+                feature, label = self._prep(batch)
+                last = (iter_id + 1) % self.accum_step == 0
+                if self.accum_step == 1:
+                    loss, prob = self.step_fn(feature, label)
+                else:
+                    r = self.run_batch(feature, label)
+                    (r["loss"] / self.accum_step).backward()
+                    loss = r["loss"]
+                    if last:
+                        self.bucketer.finish()
+                        self.optimizer.step()
+                        self.store.zero_grad()
+                if last:
+                    t += 1
+                    self.scheduler.step()
+                    if t % self.log_step == 0:
+                        li = loss.item()
+                        stat.update(li)
+                        dt = time.time() - t0
+                        self.logger("| epoch {:2d} | step {:4d} | lr {:.4E} | Train Loss Avg {:3.5f} | clips/s {:.2f}"
+                                    .format(epoch, t, self.optimizer.param_groups[0]["lr"], stat.avg,
+                                            self.log_step * self.accum_step * self.batch_size / max(dt, 1e-9)))
+                        t0 = time.time()
+                    if self.model_save and (t + 1) % self.model_save == 0 and last:
+                        os.makedirs("checkpoints", exist_ok=True)
+                        self.save_ckpt(f"./checkpoints/VST_deepfake_modality{self.modality}_batch{self.batch_size}"
+                                       f"_epoch{epoch}_step{t}.pth", epoch)
+            self.logger(f"Phase:train, Avg Loss:{stat.avg}")
+            stat.reset()
+            if self.valloader is not None:
+                t = self.eval(self.valloader, epoch, t, self.optimizer.param_groups[0]["lr"])

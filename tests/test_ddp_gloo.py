@@ -1,0 +1,79 @@
+"""CPU, world_size 2 (gloo): the flat-buffer gradient bucketer reproduces the
+single-process gradient of the global batch (mean loss), both with the
+overlapped hook path and the non-overlapped path, tolerates parameters that
+never receive a gradient (Audio2D.classifier, Q10), and broadcasts buffers."""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from deepfake_amd.ddp import GradBucketer
+from deepfake_amd.params import ParamStore
+
+
+class Net(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(16, 32)
+        self.b = torch.nn.Linear(32, 8)
+        self.unused = torch.nn.Linear(4, 4)         # never used: grad stays 0 (Q10)
+        self.bn = torch.nn.BatchNorm1d(8)
+
+    def forward(self, x):
+        return self.bn(self.b(torch.relu(self.a(x)))).sum(-1)
+
+
+def _data(seed, n):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, 16, generator=g), torch.randn(n, generator=g)
+
+
+def _worker(rank, world, port, overlap, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m = Net()
+    store = ParamStore(m, torch.float32, device=torch.device("cpu"))
+    bk = GradBucketer(store, bucket_mb=0.0002)  # tiny buckets (~52 floats) -> several buckets
+    assert len(bk.buckets) >= 2
+    bk.overlap = overlap                        # non-overlapped: hooks off, one reduce pass after backward
+    x, y = _data(1, 8)
+    xs, ys = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
+    loss = ((m(xs) - ys) ** 2).mean()
+    loss.backward()
+    if overlap:
+        bk.finish()
+    else:
+        bk.allreduce_all()
+    if rank == 0:
+        m.bn.running_mean.fill_(3.0)
+    bk.broadcast_buffers(m)
+    q.put((rank, store.grad.clone(), m.bn.running_mean.clone()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_bucketed_allreduce_matches_global_batch(overlap):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (7 if overlap else 9)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, overlap, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, rm)) for r, g, rm in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+    # reference: per-shard BN statistics, gradient averaged over the 2 shards (= DDP semantics)
+    torch.manual_seed(0)
+    m = Net()
+    store = ParamStore(m, torch.float32, device=torch.device("cpu"))
+    x, y = _data(1, 8)
+    for r in range(2):
+        loss = ((m(x[r * 4:(r + 1) * 4]) - y[r * 4:(r + 1) * 4]) ** 2).mean() / 2
+        loss.backward()
+    ref = store.grad
+    for r in range(2):
+        assert torch.allclose(res[r][0], ref, atol=1e-6), (r, (res[r][0] - ref).abs().max())
+        assert torch.all(res[r][1] == 3.0)
