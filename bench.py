@@ -41,7 +41,7 @@ def parse():
     p.add_argument("--config", default="c2")
     p.add_argument("--batch", type=int, default=8)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--graph", action="store_true", help="capture the whole step in one HIP graph (experimental)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--roofline-iters", type=int, default=20)
@@ -157,7 +157,7 @@ def main():
         dist.broadcast(store.flat, 0)
         store.refresh_shadow()
     opt = FusedSGD(store, lr=1e-4, momentum=0.9, weight_decay=1e-3)
-    step = TrainStep(model, store, opt, bucketer, graph=not a.no_graph)
+    step = TrainStep(model, store, opt, bucketer, graph=a.graph)
     feature, label = synthetic_batch(cfg, a.batch, device, 1234 + rank)
 
     for _ in range(max(a.warmup, 1)):
@@ -198,7 +198,7 @@ def main():
             "config": {"workload": f"{a.config.upper()}: Swin-T video 32x224x224 (window 8x7x7) + SwinV2 mel 224 + "
                                    f"wav2vec2-base 4s@16kHz + FusionModel, full train step",
                        "global_batch": world * a.batch, "per_gpu_batch": a.batch,
-                       "parallelism": f"dp{world}", "hip_graph": not a.no_graph, "loss": round(lossv, 5)},
+                       "parallelism": f"dp{world}", "hip_graph": a.graph, "loss": round(lossv, 5)},
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2) if train_gflop else None,
             "roofline": roof, "cpu_baseline": cpu,
         }

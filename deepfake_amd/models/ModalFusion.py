@@ -53,7 +53,8 @@ class FusionModel(nn.Module):
         feat = self.norm(Fn.linear(out.contiguous(), self.attn_proj.weight))
         feat = self.drop(feat)
         z = self.classify(feat)
-        self.last_logits = z
+        # detached: holding the graph would pin AccumulateGrad nodes to this step's stream (breaks graph capture)
+        self.last_logits = z.detach()
         return self.out_act(z.squeeze())
 
     def forward(self, feature: tuple):
