@@ -5,7 +5,8 @@ GPU0 and rooted reduce-add of gradients).
 
 One process per GPU.  Gradients live in the ParamStore's flat fp32 buffer
 (reverse registration order ~ backward order), cut into ~bucket_mb buckets.
-A post-accumulate-grad hook per parameter counts arrivals; when a bucket is
+A post-accumulate-grad hook per parameter (or, for gradients the HIP kernels
+write directly into the flat buffer, ParamStore.grad_ready) counts arrivals; when a bucket is
 complete its slice is all-reduced asynchronously (RCCL runs on its own stream
 and overlaps the rest of backward).  ``finish()`` waits for the buckets and
 averages (sum / world, matching the mean BCE loss over the global batch).
@@ -48,6 +49,7 @@ class GradBucketer:
         if self.enabled:
             for i, p in enumerate(store.params):
                 self.hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+            store.listeners.append(self._ready)    # direct-mode gradients (no AccumulateGrad)
         self.reset()
 
     def reset(self):
@@ -55,15 +57,16 @@ class GradBucketer:
             self.pending[b] = len(idx)
             self.works[b] = None
 
+    def _ready(self, i):
+        if not self.overlap:
+            return
+        b = self.bucket_of[i]
+        self.pending[b] -= 1
+        if self.pending[b] == 0 and self.works[b] is None:
+            self._launch(b)
+
     def _make_hook(self, i):
-        def hook(_p):
-            if not self.overlap:
-                return
-            b = self.bucket_of[i]
-            self.pending[b] -= 1
-            if self.pending[b] == 0 and self.works[b] is None:
-                self._launch(b)
-        return hook
+        return lambda _p: self._ready(i)
 
     def _launch(self, b):
         s, e, _ = self.buckets[b]

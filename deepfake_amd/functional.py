@@ -26,6 +26,41 @@ def _f32_zeros(p):
     return torch.zeros(p.shape, device=p.device, dtype=torch.float32)
 
 
+def _store(p):
+    return getattr(p, "_dfk_store", None) if p is not None else None
+
+
+def grad_use(ctx, idx, p):
+    """Forward side of a direct-gradient parameter: count this use so that the
+    last backward contribution (grad_done) is the one that reports p ready."""
+    st = _store(p)
+    if st is not None and ctx.needs_input_grad[idx]:
+        st.uses[id(p)] = st.uses.get(id(p), 0) + 1
+
+
+def grad_sink(p):
+    """fp32 buffer a backward kernel accumulates parameter p's gradient into.
+    With a ParamStore in direct mode this is p.grad itself (a view of the flat
+    gradient buffer, zeroed once per step): the kernels' fp32 atomics add
+    straight into it and autograd never runs a fill or AccumulateGrad add for p."""
+    st = _store(p)
+    if st is not None:
+        if p.grad is None:
+            st.rebind_grads()
+        return p.grad
+    return _f32_zeros(p)
+
+
+def grad_done(p, g):
+    """Value to return to autograd for p, after its kernels accumulated into g
+    (None in direct mode: the gradient is already in p.grad)."""
+    st = _store(p)
+    if st is None:
+        return g
+    st.grad_ready(p)
+    return None
+
+
 def rows2d(x):
     return x.reshape(-1, x.shape[-1])
 
@@ -40,25 +75,27 @@ class LinearFn(torch.autograd.Function):
         b = compute_weight(bias, dt)
         aux = torch.empty(x.shape[0], weight.shape[0], device=x.device, dtype=dt) if act == 1 else None
         y = K.linear(x, w, b, act=act, aux=aux, residual=residual)
-        ctx.save_for_backward(x, weight, aux)
+        grad_use(ctx, 1, weight)
+        grad_use(ctx, 2, bias)
+        ctx.save_for_backward(x, weight, bias, aux)
         ctx.act, ctx.has_bias, ctx.has_res = act, bias is not None, residual is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, aux = ctx.saved_tensors
+        x, weight, bias, aux = ctx.saved_tensors
         dy = dy.contiguous()
         dz = K.gelu_bwd(dy, aux) if ctx.act == 1 else dy
         w = compute_weight(weight, x.dtype)
         dx = K.linear_dx(dz, w) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = _f32_zeros(weight)
-            K.linear_dw(dz, x, dw)
+            dw = K.linear_dw(dz, x, grad_sink(weight))
+            dw = grad_done(weight, dw)
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = torch.zeros(weight.shape[0], device=x.device, dtype=torch.float32)
-            K.colsum(dz, db)
+            db = K.colsum(dz, grad_sink(bias))
+            db = grad_done(bias, db)
         return dx, dw, db, None, (dy if ctx.has_res else None)
 
 
@@ -80,25 +117,23 @@ class MlpFn(torch.autograd.Function):
         pre = torch.empty(x.shape[0], w1.shape[0], device=x.device, dtype=dt)
         h = K.linear(x, W1, B1, act=1, aux=pre)
         y = K.linear(h, W2, B2, residual=residual)
-        ctx.save_for_backward(x, w1, w2, pre, h)
+        for i, p in enumerate((w1, b1, w2, b2)):
+            grad_use(ctx, 1 + i, p)
+        ctx.save_for_backward(x, w1, b1, w2, b2, pre, h)
         ctx.has_res = residual is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w1, w2, pre, h = ctx.saved_tensors
+        x, w1, b1, w2, b2, pre, h = ctx.saved_tensors
         dy = dy.contiguous()
         dt = x.dtype
         dpre = K.linear_dx(dy, compute_weight(w2, dt), act=2, aux=pre)      # (dy W2) * gelu'(pre)
-        dw2 = _f32_zeros(w2)
-        K.linear_dw(dy, h, dw2)
-        db2 = torch.zeros(w2.shape[0], device=x.device)
-        K.colsum(dy, db2)
+        dw2 = grad_done(w2, K.linear_dw(dy, h, grad_sink(w2)))
+        db2 = grad_done(b2, K.colsum(dy, grad_sink(b2)))
         dx = K.linear_dx(dpre, compute_weight(w1, dt)) if ctx.needs_input_grad[0] else None
-        dw1 = _f32_zeros(w1)
-        K.linear_dw(dpre, x, dw1)
-        db1 = torch.zeros(w1.shape[0], device=x.device)
-        K.colsum(dpre, db1)
+        dw1 = grad_done(w1, K.linear_dw(dpre, x, grad_sink(w1)))
+        db1 = grad_done(b1, K.colsum(dpre, grad_sink(b1)))
         return dx, dw1, db1, dw2, db2, (dy if ctx.has_res else None)
 
 
@@ -114,16 +149,17 @@ class LayerNormFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, eps):
         dt = x.dtype
         y, mean, rstd = K.layernorm_fwd(x, compute_weight(weight, dt), compute_weight(bias, dt), eps)
-        ctx.save_for_backward(x, weight, mean, rstd)
+        grad_use(ctx, 1, weight)
+        grad_use(ctx, 2, bias)
+        ctx.save_for_backward(x, weight, bias, mean, rstd)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, mean, rstd = ctx.saved_tensors
-        dw = torch.zeros(weight.shape, device=x.device)
-        db = torch.zeros(weight.shape, device=x.device)
+        x, weight, bias, mean, rstd = ctx.saved_tensors
+        dw, db = grad_sink(weight), grad_sink(bias)
         dx = K.layernorm_bwd(dy.contiguous(), x, compute_weight(weight, x.dtype), mean, rstd, dw, db)
-        return dx, dw, db, None
+        return dx, grad_done(weight, dw), grad_done(bias, db), None
 
 
 def layer_norm(x, ln):
@@ -148,23 +184,31 @@ class WindowAttnFn(torch.autograd.Function):
         rpb_f = rpb.detach().float().contiguous() if rpb is not None else None
         out, lse = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], qkv.stride(0), dims, window, full_window, shift, heads,
                                hd, scale, rpb=rpb_f, pads=pads, mask=mask)
-        ctx.save_for_backward(qkv, out, lse, rpb_f, mask)
+        grad_use(ctx, 1, rpb)
+        grad_use(ctx, 2, qkv_bias)
+        ctx.save_for_backward(qkv, out, lse, rpb_f, mask, rpb, qkv_bias)
         ctx.pads, ctx.geo = pads, geo
         ctx.has_rpb, ctx.has_bias = rpb is not None, qkv_bias is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, out, lse, rpb_f, mask = ctx.saved_tensors
+        qkv, out, lse, rpb_f, mask, rpb, qkv_bias = ctx.saved_tensors
         dims, window, full_window, shift, heads, hd, scale = ctx.geo
         C = heads * hd
         dqkv = torch.empty_like(qkv)
-        drpb = torch.zeros_like(rpb_f) if ctx.has_rpb else None
-        dpads = [torch.zeros(C, device=qkv.device) for _ in range(3)] if ctx.has_bias else None
+        drpb = None
+        if ctx.has_rpb:
+            drpb = grad_sink(rpb) if rpb.dtype == torch.float32 and rpb.is_contiguous() else torch.zeros_like(rpb_f)
+        dbias = grad_sink(qkv_bias) if ctx.has_bias else None
+        dpads = [dbias[i * C:(i + 1) * C] for i in range(3)] if ctx.has_bias else None
         K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, qkv.stride(0), dims, window, full_window, shift, heads,
                      hd, scale, rpb_f, ctx.pads), dout.contiguous(), dqkv, dqkv[:, C:], dqkv[:, 2 * C:], qkv.stride(0),
                     drpb=drpb, dpads=dpads, mask=mask)
-        dbias = torch.cat(dpads) if ctx.has_bias else None
+        if ctx.has_rpb:
+            drpb = grad_done(rpb, drpb)
+        if ctx.has_bias:
+            dbias = grad_done(qkv_bias, dbias)
         return dqkv, drpb, dbias, None, None
 
 
@@ -208,19 +252,19 @@ class W2VConv0Fn(torch.autograd.Function):
         w = weight.detach().float().reshape(512, 10).contiguous()
         out, stats = K.w2v_conv0_fwd(wave.float().contiguous(), w, gamma.detach().float(), beta.detach().float(), eps,
                                      dtype)
-        ctx.save_for_backward(wave, w, gamma, beta, stats)
+        for i, p in enumerate((weight, gamma, beta)):
+            grad_use(ctx, 1 + i, p)
+        ctx.save_for_backward(wave, w, weight, gamma, beta, stats)
         ctx.eps = eps
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        wave, w, gamma, beta, stats = ctx.saved_tensors
-        dw = torch.zeros(512, 10, device=wave.device)
-        dg = torch.zeros(512, device=wave.device)
-        db = torch.zeros(512, device=wave.device)
+        wave, w, weight, gamma, beta, stats = ctx.saved_tensors
+        dw, dg, db = grad_sink(weight), grad_sink(gamma), grad_sink(beta)
         K.w2v_conv0_bwd(wave.float().contiguous(), w, gamma.detach().float(), beta.detach().float(), ctx.eps, stats,
-                        dout.contiguous(), dw, dg, db)
-        return None, dw.view(512, 1, 10), dg, db, None, None
+                        dout.contiguous(), dw.view(512, 10), dg, db)
+        return None, grad_done(weight, dw), grad_done(gamma, dg), grad_done(beta, db), None, None
 
 
 class ConvGeluFn(torch.autograd.Function):
@@ -283,13 +327,14 @@ class PosConvFn(torch.autograd.Function):
         K.gemm(x, C, False, w2, k * Cg, False, T, Cg, k * Cg, y, C, dtype=K.L.dt(x), bias=compute_weight(bias, dt),
                bias_bs1=Cg, act=1, aux=pre, ldaux=C, residual=x, ldr=C, nz=(B, groups), a_bs=(T * C, Cg),
                b_bs=(0, Cg * k * Cg), c_bs=(T * C, Cg), r_bs=(T * C, Cg), a_conv=(Cg, 1, pad, T))
-        ctx.save_for_backward(x, weight, pre)
+        grad_use(ctx, 2, bias)
+        ctx.save_for_backward(x, weight, bias, pre)
         ctx.groups = groups
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, pre = ctx.saved_tensors
+        x, weight, bias, pre = ctx.saved_tensors
         B, T, C = x.shape
         G = ctx.groups
         Cg = C // G
@@ -297,8 +342,7 @@ class PosConvFn(torch.autograd.Function):
         dt = K.L.dt(x)
         dy = dy.contiguous()
         dpre = K.gelu_bwd(dy, pre)
-        db = torch.zeros(C, device=x.device)
-        K.colsum(dpre.view(-1, C), db)
+        db = grad_done(bias, K.colsum(dpre.view(-1, C), grad_sink(bias)))
         dw2 = torch.zeros(C, k * Cg, device=x.device)
         K.gemm(dpre, C, True, x, C, True, Cg, k * Cg, T, dw2, k * Cg, dtype=dt, c_f32=True, atomic=True,
                splitk=2, nz=(B, G), a_bs=(T * C, Cg), b_bs=(T * C, Cg), c_bs=(0, Cg * k * Cg),
@@ -347,16 +391,17 @@ class PatchEmbedFn(torch.autograd.Function):
         cols, grid = K.patch_im2col(x, layout, patch, dtype)
         W = compute_weight(weight, dtype).reshape(weight.shape[0], -1)
         y = K.linear(cols, W, compute_weight(bias, dtype))
-        ctx.save_for_backward(cols, weight)
+        grad_use(ctx, 1, weight)
+        grad_use(ctx, 2, bias)
+        ctx.save_for_backward(cols, weight, bias)
         ctx.grid = grid
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        cols, weight = ctx.saved_tensors
+        cols, weight, bias = ctx.saved_tensors
         dy = dy.contiguous()
-        dw = torch.zeros(weight.shape[0], cols.shape[1], device=dy.device)
-        K.linear_dw(dy, cols, dw)
-        db = torch.zeros(weight.shape[0], device=dy.device)
-        K.colsum(dy, db)
-        return None, dw.view(weight.shape), db, None, None, None
+        dw = grad_sink(weight)
+        K.linear_dw(dy, cols, dw.view(weight.shape[0], -1))
+        db = grad_done(bias, K.colsum(dy, grad_sink(bias)))
+        return None, grad_done(weight, dw), db, None, None, None

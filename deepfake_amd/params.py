@@ -6,6 +6,12 @@ place and buckets of the flat buffer are all-reduced as-is, no copies), and —
 in bf16 compute mode — a bf16 shadow view (``p._dfk_shadow``) that the GEMMs
 read.  The fused SGD kernel updates the fp32 master and rewrites the shadow in
 the same pass, so no separate cast kernel runs per step.
+
+Direct mode (default): the HIP backward kernels accumulate weight gradients
+straight into ``p.grad`` with fp32 atomics (deepfake_amd.functional.grad_sink)
+and report the parameter ready through ``grad_ready`` — autograd then runs no
+per-parameter zero-fill or AccumulateGrad add (~1600 small kernels per C2 step).
+Parameters reached only through torch ops keep the AccumulateGrad path.
 Parameters are laid out in *reverse* registration order, which is roughly the
 order in which backward produces their gradients (buckets in
 reverse registration order), and each is 16-B aligned.
@@ -18,7 +24,7 @@ _ALIGN = 8  # elements (bf16 shadow views stay 16-B aligned)
 
 
 class ParamStore:
-    def __init__(self, model, compute_dtype=torch.float32, device=None):
+    def __init__(self, model, compute_dtype=torch.float32, device=None, direct=True):
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.params.reverse()
         dev = device or self.params[0].device
@@ -39,7 +45,24 @@ class ParamStore:
                 p.grad = self.grad[o:o + p.numel()].view_as(p)
                 if self.shadow is not None:
                     p._dfk_shadow = self.shadow[o:o + p.numel()].view_as(p)
+                if direct:
+                    p._dfk_store = self
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.uses = {}           # id(p) -> forward uses whose backward has not run yet (direct mode)
+        self.listeners = []      # callbacks(i) when parameter i's gradient is complete
         self.refresh_shadow()
+
+    def grad_ready(self, p):
+        """A direct-mode backward finished accumulating into p.grad."""
+        k = id(p)
+        n = self.uses.get(k, 1) - 1
+        if n > 0:
+            self.uses[k] = n
+            return
+        self.uses.pop(k, None)
+        i = self.index[k]
+        for cb in self.listeners:
+            cb(i)
 
     def refresh_shadow(self):
         if self.shadow is not None:
@@ -48,6 +71,7 @@ class ParamStore:
 
     def zero_grad(self):
         self.grad.zero_()
+        self.uses.clear()
 
     def rebind_grads(self):
         """Re-attach .grad views (a user may have set grads to None)."""

@@ -65,3 +65,37 @@ def test_fused_c1_train_step(dt, tol):
         ref = float(fx[k])
         got = float(names[k[3:]].detach().double().sum())
         assert abs(got - ref) <= 1e-4 * max(1.0, abs(ref)) + 1e-3, (k, got, ref)
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float32, 2e-3), (torch.bfloat16, 1.5e-1)])
+def test_fused_c1_train_step_flat_store(dt, tol):
+    """Same step through the training runtime: flat ParamStore in direct-gradient
+    mode (HIP backward kernels accumulate into the flat fp32 gradient buffer)
+    and the fused SGD kernel (fp32 master + bf16 shadow)."""
+    from deepfake_amd.optim import FusedSGD
+    from deepfake_amd.params import ParamStore
+    c, m, x, label = _model(dt)
+    fx = load(c["name"])
+    m.train()
+    store = ParamStore(m, dt)
+    opt = FusedSGD(store, lr=c["lr"], momentum=0.9, weight_decay=c["wd"])
+    store.zero_grad()
+    p = m(x)
+    loss = torch.nn.BCELoss()(p.float(), label)
+    loss.backward()
+    assert not store.uses, "a direct-mode parameter never reported its gradient"
+    assert abs(loss.item() - float(fx["loss"])) < tol * abs(float(fx["loss"]))
+    names = dict(m.named_parameters())
+    bad = []
+    for k in keys(fx, "gn:"):
+        ref = float(fx[k])
+        got = float(names[k[3:]].grad.norm())
+        if abs(got - ref) > tol * ref + (1e-6 if dt == torch.float32 else 1e-5):
+            bad.append((k[3:], got, ref))
+    assert not bad, bad[:8]
+    opt.step()
+    torch.cuda.synchronize()
+    for k in keys(fx, "ps:"):
+        ref = float(fx[k])
+        got = float(names[k[3:]].detach().double().sum())
+        assert abs(got - ref) <= 1e-4 * max(1.0, abs(ref)) + 1e-3, (k, got, ref)
