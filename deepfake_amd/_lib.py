@@ -47,7 +47,7 @@ class WattnArgs(C.Structure):
 class WattnBwdArgs(C.Structure):
     _fields_ = [("f", WattnArgs), ("dout", C.c_void_p), ("dq", C.c_void_p), ("dk", C.c_void_p),
                 ("dv", C.c_void_p), ("drpb", C.c_void_p), ("dpad_q", C.c_void_p), ("dpad_k", C.c_void_p),
-                ("dpad_v", C.c_void_p), ("ld_dqkv", C.c_int64), ("ld_dout", C.c_int64)]
+                ("dpad_v", C.c_void_p), ("ld_dqkv", C.c_int64), ("ld_dout", C.c_int64), ("ws", C.c_void_p)]
 
 
 class Im2colArgs(C.Structure):
@@ -66,6 +66,7 @@ SIGNATURES = {
     "dfk_layernorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, C.c_int, C.c_int, _VP],
     "dfk_wattn_fwd": [C.POINTER(WattnArgs), _VP],
     "dfk_wattn_bwd": [C.POINTER(WattnBwdArgs), _VP],
+    "dfk_wattn_bwd_workspace": [C.POINTER(WattnArgs)],
     "dfk_patch_im2col": [_VP, C.c_int, _VP, C.c_int, C.POINTER(Im2colArgs), _VP],
     "dfk_patch_merge": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],
     "dfk_rowmean": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],
@@ -79,6 +80,7 @@ SIGNATURES = {
 }
 
 _lib = None
+RESTYPES = {"dfk_wattn_bwd_workspace": _I64}
 
 
 def lib():
@@ -90,7 +92,7 @@ def lib():
         L = C.CDLL(LIB_PATH)
         for name, argt in SIGNATURES.items():
             fn = getattr(L, name)
-            fn.restype = C.c_int
+            fn.restype = RESTYPES.get(name, C.c_int)
             fn.argtypes = argt
         _lib = L
     return _lib

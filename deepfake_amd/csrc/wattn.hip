@@ -334,6 +334,39 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
 // flushed with one global atomic per entry.
 namespace {
 
+// this window-head's dRPB partial -> its workspace row (reduced by drpb_reduce_kernel);
+// without a workspace, device-scope atomics on the shared [L,nH] table
+__device__ __forceinline__ void flush_drpb(const dfk_wattn_bwd_args& ba, const Geo& g, const float* drpb, int head,
+                                           int accum, int tid, int nthreads) {
+  if (ba.ws) {
+    float* w = ba.ws + (long)blockIdx.x * ((g.L + 3) & ~3);
+    for (int l = tid; l < g.L; l += nthreads) w[l] = accum ? w[l] + drpb[l] : drpb[l];
+  } else {
+    for (int l = tid; l < g.L; l += nthreads)
+      if (drpb[l] != 0.f) atomicAdd(ba.drpb + (long)l * ba.f.heads + head, drpb[l]);
+  }
+}
+
+// drpb[l][h] += sum over window-heads u = h (mod heads) of ws[u][l]; 16 row phases per 64 entries
+__global__ __launch_bounds__(1024) void drpb_reduce_kernel(const float* __restrict__ ws, long units, int heads, int L,
+                                                           float* __restrict__ drpb) {
+  __shared__ float part[16][64];
+  const int Lal = (L + 3) & ~3;
+  const int c = threadIdx.x & 63, ph = threadIdx.x >> 6, h = blockIdx.y;
+  const int l = blockIdx.x * 64 + c;
+  float s = 0.f;
+  if (l < L)
+    for (long u = h + (long)heads * ph; u < units; u += (long)heads * 16) s += ws[u * Lal + l];
+  part[ph][c] = s;
+  __syncthreads();
+  if (ph == 0 && l < L) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += part[i][c];
+    drpb[(long)l * heads + h] += t;
+  }
+}
+
 template <typename T, int HD>
 __global__ __launch_bounds__(256) void wattn_bwd_kernel(const dfk_wattn_bwd_args ba, const Geo g, int q0, int Qn,
                                                         int accum_kv) {
@@ -598,9 +631,398 @@ __global__ __launch_bounds__(256) void wattn_bwd_kernel(const dfk_wattn_bwd_args
     if (t.row >= 0) stf<T>(reinterpret_cast<T*>(ba.dq) + (long)t.row * ba.ld_dqkv + hoff + e, dQacc[idx]);
     else if (t.row == -1 && ba.dpad_q) atomicAdd(ba.dpad_q + hoff + e, dQacc[idx]);
   }
-  if (ba.drpb)
-    for (int l = tid; l < g.L; l += 256)
-      if (drpb[l] != 0.f) atomicAdd(ba.drpb + (long)l * a.heads + head, drpb[l]);
+  if (a.rpb && ba.drpb) flush_drpb(ba, g, drpb, head, accum_kv, tid, 256);
+}
+
+// ------------------------------------------------------------ bf16 backward
+// Same decomposition (key-owner waves, dK/dV in registers, dQ and dRPB in LDS
+// fp32), re-laid for latency: up to 8 waves per window-head (2 waves / SIMD),
+// per-query statistics (packed pos|label, lse, delta) fetched once per 32-query
+// block as 16-B vectors, softmax in base 2 with no data-dependent branches,
+// the dO / Q operands of dV = P^T dO and dK = dS^T Q read with ds_read_tr16
+// from XOR-swizzled tiles, dS crossing the wave's scratch as dS^T (b64 stores,
+// tr16 loads), and a bank-swizzled dQ accumulator.
+
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v lds_short4;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr int kBwdWaves = 8;
+constexpr int kSdStride = 40;  // bf16 row stride of the per-wave dS^T scratch [32 keys][32 queries]
+
+// element offset of (row, col) in a [rows][HD] bf16 tile with 16-B chunks XOR-swizzled by row:
+// conflict-free 16-B row reads (A operands) and 8-B transposed reads (tr16 B operands)
+template <int HD>
+__device__ __forceinline__ int swz(int row, int col) {
+  const int f = HD == 32 ? ((row & 2) | ((row >> 2) & 1)) : (((row & 3) << 1) | ((row >> 2) & 1));
+  return row * HD + (((col >> 3) ^ f) << 3) + (col & 7);
+}
+
+// fp32 [rows][HD] accumulator: the 4 rows a C fragment touches land in two bank halves
+template <int HD>
+__device__ __forceinline__ int dq_off(int row, int col) {
+  return row * HD + (col ^ (((row >> 2) & 1) << 4));
+}
+
+__device__ __forceinline__ bf16x8 tr16x2(const bf16raw* p0, const bf16raw* p1) {
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(p0));
+  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(p1));
+  short8 u = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+__device__ __forceinline__ float dot8_bf16(uint4 x, uint4 y) {
+  const bf16raw* a = reinterpret_cast<const bf16raw*>(&x);
+  const bf16raw* b = reinterpret_cast<const bf16raw*>(&y);
+  float d = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d += bf2f(a[j]) * bf2f(b[j]);
+  return d;
+}
+
+template <int HD, bool RPB, bool MASK>
+__global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(const dfk_wattn_bwd_args ba, const Geo g,
+                                                                              int q0, int Qn, int accum_kv,
+                                                                              bf16raw* __restrict__ dsg) {
+  // One workgroup = one (clip, window, head); wave w owns key blocks w, w + nwaves (dK, dV in registers).
+  // All waves step through the query blocks together: per 32-query block each wave computes S, dP, P, dS
+  // for its keys, accumulates dV += P^T dO and dK += dS^T Q, and its partial dQ = dS K; the partials are
+  // summed through LDS (plain stores, one barrier pair per block) and the finished dQ rows stored.
+  // dS^T also goes to global scratch (dsg) for the deterministic dRPB reduction.  No LDS atomics.
+  const dfk_wattn_args& a = ba.f;
+  constexpr int kDqStride = HD + 4;  // fp32 row stride of the per-wave dQ partials [32 queries][HD]
+  const int nwaves = blockDim.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Lal = (g.L + 3) & ~3;
+  char* p = smem;
+  int* trow = reinterpret_cast<int*>(p); p += 4 * g.Np;
+  int* tpk = reinterpret_cast<int*>(p); p += 4 * g.Np;          // pos << 5 | region label
+  float* rpb2 = reinterpret_cast<float*>(p); p += 4 * Lal;      // rpb * log2(e)
+  float* lse2 = reinterpret_cast<float*>(p); p += 4 * Qn;       // lse * log2(e); +inf beyond N
+  float* delta = reinterpret_cast<float*>(p); p += 4 * Qn;
+  float* dQp = reinterpret_cast<float*>(p); p += 4 * (size_t)nwaves * 32 * kDqStride;  // per-wave dQ partials
+  bf16raw* Qs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Qn * HD;
+  bf16raw* dOs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Qn * HD;
+  bf16raw* Sd = reinterpret_cast<bf16raw*>(p);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = lane >> 4, ql = lane & 15, tq = ql >> 2, tp = ql & 3;
+  int unit = blockIdx.x;
+  const int head = unit % a.heads;
+  unit /= a.heads;
+  const int win = unit % g.nW, b = unit / g.nW;
+  const float* mrow = MASK ? a.mask + (((long)b * g.nW + win) % a.mask_nw) * g.N * g.N : nullptr;
+  const int hoff = head * HD;
+  const bf16raw* og = reinterpret_cast<const bf16raw*>(a.out);
+  const bf16raw* dog = reinterpret_cast<const bf16raw*>(ba.dout);
+  const bf16raw* qg = reinterpret_cast<const bf16raw*>(a.q);
+
+  for (int i = tid; i < g.Np; i += blockDim.x) {
+    const TokInfo t = token_info(a, g, b, win, i);
+    trow[i] = t.row;
+    tpk[i] = (t.pos << 5) | (t.lab & 31);
+  }
+  if (RPB)
+    for (int l = tid; l < g.L; l += blockDim.x) rpb2[l] = a.rpb[(long)l * a.heads + head] * kLog2e;
+  for (int li = tid; li < Qn; li += blockDim.x) {
+    const int i = q0 + li;
+    lse2[li] = i < g.N ? a.lse[(long)blockIdx.x * g.Np + i] * kLog2e : INFINITY;
+  }
+  __syncthreads();
+  // Q, dO rows -> swizzled LDS tiles; delta = rowsum(O * dO) (CH lanes per row)
+  constexpr int CH = HD / 8;
+  for (int base = 0; base < Qn * CH; base += blockDim.x) {
+    const int idx = base + tid;
+    float d = 0.f;
+    if (idx < Qn * CH) {
+      const int li = idx / CH, c = (idx % CH) * 8;
+      const int row = trow[q0 + li];
+      const bf16raw* qp = row >= 0 ? qg + (long)row * a.ld_qkv + hoff + c
+                                   : (row == -1 && a.pad_q ? reinterpret_cast<const bf16raw*>(a.pad_q) + hoff + c
+                                                           : nullptr);
+      uint4 dv = make_uint4(0, 0, 0, 0);
+      if (row >= 0) {
+        dv = *reinterpret_cast<const uint4*>(dog + (long)row * ba.ld_dout + hoff + c);
+        d = dot8_bf16(*reinterpret_cast<const uint4*>(og + (long)row * a.ld_out + hoff + c), dv);
+      }
+      *reinterpret_cast<uint4*>(Qs + swz<HD>(li, c)) = ld16<bf16raw>(qp);
+      *reinterpret_cast<uint4*>(dOs + swz<HD>(li, c)) = dv;
+    }
+#pragma unroll
+    for (int o = 1; o < CH; o <<= 1) d += __shfl_xor(d, o, 64);
+    if (idx < Qn * CH && (idx % CH) == 0) delta[idx / CH] = d;
+  }
+
+  __syncthreads();
+
+  // ---- passes over the key blocks: in pass p, wave w owns key block p*nwaves + w
+  const int nkb = g.Np / 32, nqb = Qn / 32;
+  bf16raw* Sw = Sd + wave * 32 * kSdStride;
+  float* myQ = dQp + wave * 32 * kDqStride;
+  const float scale2 = a.scale * kLog2e;
+  const float mpen = -100.f * kLog2e;
+  bf16raw* dsu = RPB && dsg ? dsg + (long)blockIdx.x * g.Np * g.Np : nullptr;   // this window-head's dS^T [k][q]
+  for (int pass = 0; pass * nwaves < nkb; ++pass) {
+    const int kb = pass * nwaves + wave;
+    const bool own = kb < nkb;
+    const int kbc = own ? kb : 0;
+    // K^T / V^T B operands (key on the lane), K natural-order B operand for dQ, key statistics
+    int kpk[2];
+    float kneg[2];
+    bf16x8 kB[2][HD / 32], vB[2][HD / 32], kN[HD / 16];
+    f32x4 dK[2][HD / 16], dV[2][HD / 16];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int k = kbc * 32 + h2 * 16 + ql;
+      const int row = trow[k];
+      kpk[h2] = tpk[k];
+      kneg[h2] = row == -2 ? -INFINITY : 0.f;
+      const bf16raw* kp = tok_ptr<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff);
+      const bf16raw* vp = tok_ptr<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff);
+#pragma unroll
+      for (int es = 0; es < HD / 32; ++es) {
+        uint4 u = kp ? *reinterpret_cast<const uint4*>(kp + es * 32 + grp * 8) : make_uint4(0, 0, 0, 0);
+        kB[h2][es] = __builtin_bit_cast(bf16x8, u);
+        u = vp ? *reinterpret_cast<const uint4*>(vp + es * 32 + grp * 8) : make_uint4(0, 0, 0, 0);
+        vB[h2][es] = __builtin_bit_cast(bf16x8, u);
+      }
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et) { dK[h2][et] = f32x4{0, 0, 0, 0}; dV[h2][et] = f32x4{0, 0, 0, 0}; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = trow[kbc * 32 + grp * 8 + j];
+      const bf16raw* kp = tok_ptr<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + ql);
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et) kN[et][j] = kp ? __builtin_bit_cast(__bf16, kp[et * 16]) : (__bf16)0.f;
+    }
+
+    for (int qb = 0; qb < nqb; ++qb) {
+      const int qr0 = qb * 32;
+      f32x4 dq[2][HD / 16];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int et = 0; et < HD / 16; ++et) dq[qh][et] = f32x4{0, 0, 0, 0};
+      if (own) {
+        // query-side operands and statistics of the block
+        f32x4 L2[2], DL[2];
+        int4 QP[2];
+        bf16x8 qa[2][HD / 32], da[2][HD / 32];
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const int r0 = qr0 + qh * 16 + grp * 4;
+          L2[qh] = *reinterpret_cast<const f32x4*>(lse2 + r0);
+          DL[qh] = *reinterpret_cast<const f32x4*>(delta + r0);
+          QP[qh] = *reinterpret_cast<const int4*>(tpk + q0 + r0);
+#pragma unroll
+          for (int es = 0; es < HD / 32; ++es) {
+            const int off = swz<HD>(qr0 + qh * 16 + ql, es * 32 + grp * 8);
+            qa[qh][es] = *reinterpret_cast<const bf16x8*>(Qs + off);
+            da[qh][es] = *reinterpret_cast<const bf16x8*>(dOs + off);
+          }
+        }
+        float bias[2][2][4];
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              bias[qh][h2][r] = RPB ? rpb2[(QP[qh][r] >> 5) - (kpk[h2] >> 5) + g.C0] : 0.f;
+        // S = Q K^T, dP = dO V^T : rows = queries, lanes = keys
+        f32x4 s[2][2], dp[2][2];
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            s[qh][h2] = f32x4{0, 0, 0, 0};
+            dp[qh][h2] = f32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int es = 0; es < HD / 32; ++es) {
+              s[qh][h2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[qh][es], kB[h2][es], s[qh][h2], 0, 0, 0);
+              dp[qh][h2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[qh][es], vB[h2][es], dp[qh][h2], 0, 0, 0);
+            }
+          }
+        // P = 2^(s*scale*log2e + bias - lse2); dS = P (dP - delta); A operands of P^T / dS^T
+        bf16x8 pa[2], sa[2];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+          for (int qh = 0; qh < 2; ++qh) {
+            float dsv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float x = s[qh][h2][r] * scale2 + (bias[qh][h2][r] + kneg[h2] - L2[qh][r]);
+              if (g.use_mask) x += ((QP[qh][r] ^ kpk[h2]) & 31) ? mpen : 0.f;
+              if constexpr (MASK) {
+                const int q = q0 + qr0 + qh * 16 + grp * 4 + r, k = kb * 32 + h2 * 16 + ql;
+                if (q < g.N && k < g.N) x += mrow[q * g.N + k] * kLog2e;
+              }
+              const float P = __builtin_amdgcn_exp2f(x);
+              const float dS = P * (dp[qh][h2][r] - DL[qh][r]);
+              pa[h2][qh * 4 + r] = (__bf16)P;
+              sa[h2][qh * 4 + r] = (__bf16)dS;
+              dsv[r] = dS;
+            }
+            uint2 w;
+            w.x = (uint32_t)f2bf(dsv[0]) | ((uint32_t)f2bf(dsv[1]) << 16);
+            w.y = (uint32_t)f2bf(dsv[2]) | ((uint32_t)f2bf(dsv[3]) << 16);
+            // dS^T -> wave scratch [32 keys][32 queries]
+            *reinterpret_cast<uint2*>(Sw + (h2 * 16 + ql) * kSdStride + qh * 16 + grp * 4) = w;
+          }
+        // dV[k][e] += P^T dO ; dK[k][e] += dS^T Q   (query slot j <-> row qr0 + (j>>2)*16 + 4grp + (j&3))
+#pragma unroll
+        for (int et = 0; et < HD / 16; ++et) {
+          const int c = et * 16 + tp * 4;
+          const int rlo = qr0 + grp * 4 + tq, rhi = rlo + 16;
+          const bf16x8 dob = tr16x2(dOs + swz<HD>(rlo, c), dOs + swz<HD>(rhi, c));
+          const bf16x8 qbv = tr16x2(Qs + swz<HD>(rlo, c), Qs + swz<HD>(rhi, c));
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            dV[h2][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[h2], dob, dV[h2][et], 0, 0, 0);
+            dK[h2][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa[h2], qbv, dK[h2][et], 0, 0, 0);
+          }
+        }
+        asm volatile("" ::: "memory");
+        // partial dQ[q][e] = dS K over this key block (dS rows via tr16 from the scratch, keys in natural order)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const bf16x8 sq = tr16x2(Sw + (grp * 8 + tq) * kSdStride + qh * 16 + tp * 4,
+                                   Sw + (grp * 8 + 4 + tq) * kSdStride + qh * 16 + tp * 4);
+#pragma unroll
+          for (int et = 0; et < HD / 16; ++et)
+            dq[qh][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sq, kN[et], dq[qh][et], 0, 0, 0);
+        }
+        if (dsu) {  // scratch rows (32 keys x 64 B) -> global dS^T[k][q], 2 x 16 B per lane
+          const int kr = lane >> 1, half = lane & 1;
+          const uint4 v0 = *reinterpret_cast<const uint4*>(Sw + kr * kSdStride + half * 16);
+          const uint4 v1 = *reinterpret_cast<const uint4*>(Sw + kr * kSdStride + half * 16 + 8);
+          bf16raw* gp = dsu + (long)(kb * 32 + kr) * g.Np + q0 + qr0 + half * 16;
+          *reinterpret_cast<uint4*>(gp) = v0;
+          *reinterpret_cast<uint4*>(gp + 8) = v1;
+        }
+        asm volatile("" ::: "memory");
+      }
+      // ---- dQ block: partials -> LDS, sum over waves, store (pass 0) or add (later passes)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int et = 0; et < HD / 16; ++et)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) myQ[(qh * 16 + grp * 4 + r) * kDqStride + et * 16 + ql] = dq[qh][et][r];
+      __syncthreads();
+      const int nw = min(nwaves, nkb - pass * nwaves);
+      for (int t = tid; t < 32 * (HD / 8); t += blockDim.x) {
+        const int lr = t / (HD / 8), c = (t % (HD / 8)) * 8;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int w = 0; w < nw; ++w) {
+          const float* src = dQp + (w * 32 + lr) * kDqStride + c;
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(src), x1 = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[j] += x0[j]; v[4 + j] += x1[j]; }
+        }
+        const int i = q0 + qr0 + lr;
+        const int row = i < g.N ? trow[i] : -2;
+        if (row >= 0) {
+          bf16raw* dst = reinterpret_cast<bf16raw*>(ba.dq) + (long)row * ba.ld_dqkv + hoff + c;
+          uint4 u = pass > 0 ? *reinterpret_cast<const uint4*>(dst) : make_uint4(0, 0, 0, 0);
+          bf16raw* pe = reinterpret_cast<bf16raw*>(&u);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pe[j] = f2bf((pass > 0 ? bf2f(pe[j]) : 0.f) + v[j] * a.scale);
+          *reinterpret_cast<uint4*>(dst) = u;
+        } else if (row == -1 && ba.dpad_q) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) atomicAdd(ba.dpad_q + hoff + c + j, v[j] * a.scale);
+        }
+      }
+      __syncthreads();
+    }
+    // ---- dK (scaled), dV of the owned key block: C layout row = key 4grp+r, col = e
+    if (own) {
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = trow[kb * 32 + h2 * 16 + grp * 4 + r];
+#pragma unroll
+          for (int et = 0; et < HD / 16; ++et) {
+            const int e = hoff + et * 16 + ql;
+            const float vk = dK[h2][et][r] * a.scale, vv = dV[h2][et][r];
+            if (row >= 0) {
+              bf16raw* pk = reinterpret_cast<bf16raw*>(ba.dk) + (long)row * ba.ld_dqkv + e;
+              bf16raw* pv = reinterpret_cast<bf16raw*>(ba.dv) + (long)row * ba.ld_dqkv + e;
+              *pk = f2bf(accum_kv ? bf2f(*pk) + vk : vk);
+              *pv = f2bf(accum_kv ? bf2f(*pv) + vv : vv);
+            } else if (row == -1) {
+              if (ba.dpad_k) atomicAdd(ba.dpad_k + e, vk);
+              if (ba.dpad_v) atomicAdd(ba.dpad_v + e, vv);
+            }
+          }
+        }
+    }
+  }
+}
+
+// dRPB from the dS^T scratch: drpb[pos(q) - pos(k) + C0] += sum over windows of dS[q][k].
+// Block (chunk, head, split): 8 consecutive (k, q) elements per thread summed over the split's windows,
+// scattered into an LDS table (once per element per block), table -> one workspace row.
+__global__ __launch_bounds__(256) void drpb_from_ds_kernel(const bf16raw* __restrict__ ds, long units, int heads,
+                                                           int Np, int N, int fh, int fw, int C0, int L, int wps,
+                                                           float* __restrict__ rows) {
+  extern __shared__ float tab[];
+  const int chunk = blockIdx.x, h = blockIdx.y, split = blockIdx.z;
+  const int Lal = (L + 3) & ~3;
+  for (int l = threadIdx.x; l < L; l += blockDim.x) tab[l] = 0.f;
+  __syncthreads();
+  const long e0 = ((long)chunk * blockDim.x + threadIdx.x) * 8;
+  const long NN = (long)Np * Np;
+  if (e0 < NN) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const long nwin = units / heads;
+    const long w0 = (long)split * wps, w1 = min(nwin, w0 + wps);
+    for (long w = w0; w < w1; ++w) {
+      const uint4 v = *reinterpret_cast<const uint4*>(ds + (w * heads + h) * NN + e0);
+      const bf16raw* pe = reinterpret_cast<const bf16raw*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f(pe[j]);
+    }
+    const int k = (int)(e0 / Np), qb = (int)(e0 % Np);
+    if (k < N) {
+      auto pos = [&](int i) { return ((i / (fh * fw)) * (2 * fh - 1) + (i / fw) % fh) * (2 * fw - 1) + i % fw; };
+      const int pk = pos(k);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (qb + j < N) atomicAdd(tab + pos(qb + j) - pk + C0, acc[j]);
+    }
+  }
+  __syncthreads();
+  float* row = rows + ((long)(split * gridDim.x + chunk) * heads + h) * Lal;
+  for (int l = threadIdx.x; l < L; l += blockDim.x) row[l] = tab[l];
+}
+
+struct DsPlan {
+  long ds_elems;   // bf16 dS^T scratch elements
+  int nchunks, nsplit, wps;
+  long rows;       // workspace rows of L floats
+};
+
+DsPlan ds_plan(const dfk_wattn_args& a, const Geo& g) {
+  DsPlan pl;
+  const long units = (long)a.B * g.nW * a.heads;
+  pl.ds_elems = units * g.Np * g.Np;
+  pl.nchunks = (int)dfk_cdiv((long)g.Np * g.Np, 256 * 8);
+  const long nwin = units / a.heads;
+  pl.wps = 64;
+  pl.nsplit = (int)dfk_cdiv(nwin, pl.wps);
+  pl.rows = (long)pl.nsplit * pl.nchunks * a.heads;
+  return pl;
+}
+
+size_t bwd_lds_bf16(const dfk_wattn_args& a, const Geo& g, int Qn, int nwaves) {
+  const size_t Lal = (g.L + 3) & ~3;
+  return 8 * (size_t)g.Np + 4 * Lal + 8 * (size_t)Qn + (size_t)nwaves * 32 * (a.hd + 4) * 4 + 4 * (size_t)Qn * a.hd +
+         (size_t)nwaves * 32 * kSdStride * 2;
 }
 
 // LDS bytes for a query chunk of Qn rows
@@ -611,6 +1033,12 @@ size_t bwd_lds(const dfk_wattn_args& a, const Geo& g, int Qn) {
          es * 4 * 32 * 32;
 }
 
+void reduce_drpb(const dfk_wattn_bwd_args& ba, const Geo& g, long units, hipStream_t s) {
+  if (!ba.f.rpb || !ba.drpb || !ba.ws) return;
+  hipLaunchKernelGGL(drpb_reduce_kernel, dim3(dfk_cdiv(g.L, 64), ba.f.heads), dim3(1024), 0, s, ba.ws, units,
+                     ba.f.heads, g.L, ba.drpb);
+}
+
 }  // namespace
 
 extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
@@ -619,7 +1047,50 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
   const int vec = a.dtype == DFK_BF16 ? 8 : 4;
   if (bp->ld_dqkv % vec || bp->ld_dout % vec) return DFK_EINVAL;
   const Geo g = make_geo(a);
-  // largest query chunk (multiple of 32) that fits the 160 KiB LDS
+  if (a.dtype == DFK_BF16) {
+    const int nwaves = std::min(a.hd == 32 ? kBwdWaves : kBwdWaves / 2, g.Np / 32);  // hd 64: 4 waves, 512 VGPRs
+    int Qn = g.Np;
+    while (Qn > 32 && bwd_lds_bf16(a, g, Qn, nwaves) > 160 * 1024) Qn -= 32;
+    const size_t lds = bwd_lds_bf16(a, g, Qn, nwaves);
+    if (lds > 160 * 1024) return DFK_EINVAL;
+    const long units = (long)a.B * g.nW * a.heads;
+    if (units <= 0) return 0;
+#define LAUNCH_B16(HD, RPB, MASK)                                                                          \
+  do {                                                                                                     \
+    auto kfn = wattn_bwd_bf16_kernel<HD, RPB, MASK>;                                                       \
+    static bool attr_set = false;                                                                          \
+    if (!attr_set) {                                                                                       \
+      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      attr_set = true;                                                                                     \
+    }                                                                                                      \
+    for (int q0 = 0; q0 < g.Np; q0 += Qn)                                                                  \
+      hipLaunchKernelGGL(kfn, dim3((unsigned)units), dim3(64 * nwaves), lds, s, *bp, g, q0,                \
+                         std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0, dsg);                                    \
+  } while (0)
+#define PICK_B16(HD)                                                 \
+  do {                                                               \
+    if (a.rpb) { if (a.mask) LAUNCH_B16(HD, true, true); else LAUNCH_B16(HD, true, false); } \
+    else { if (a.mask) LAUNCH_B16(HD, false, true); else LAUNCH_B16(HD, false, false); }     \
+  } while (0)
+    const bool want_drpb = a.rpb && bp->drpb;
+    if (want_drpb && !bp->ws) return DFK_EINVAL;  // dRPB needs the dfk_wattn_bwd_workspace scratch
+    const DsPlan pl = ds_plan(a, g);
+    bf16raw* dsg = want_drpb ? reinterpret_cast<bf16raw*>(bp->ws) : nullptr;
+    if (a.hd == 32) PICK_B16(32); else PICK_B16(64);
+#undef PICK_B16
+#undef LAUNCH_B16
+    if (want_drpb) {
+      float* rows = reinterpret_cast<float*>(reinterpret_cast<char*>(bp->ws) + ((pl.ds_elems * 2 + 15) & ~15L));
+      hipLaunchKernelGGL(drpb_from_ds_kernel, dim3(pl.nchunks, a.heads, pl.nsplit), dim3(256),
+                         ((g.L + 3) & ~3) * 4, s, dsg, units, a.heads, g.Np, g.N, a.fh, a.fw, g.C0, g.L, pl.wps,
+                         rows);
+      hipLaunchKernelGGL(drpb_reduce_kernel, dim3(dfk_cdiv(g.L, 64), a.heads), dim3(1024), 0, s, rows, pl.rows,
+                         a.heads, g.L, bp->drpb);
+    }
+    DFK_CHECK_LAUNCH();
+    return 0;
+  }
+  // fp32 (parity mode): largest query chunk (multiple of 32) that fits the 160 KiB LDS
   int Qn = g.Np;
   while (Qn > 32 && bwd_lds(a, g, Qn) > 160 * 1024) Qn -= 32;
   const size_t lds = bwd_lds(a, g, Qn);
@@ -638,12 +1109,21 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     for (int q0 = 0; q0 < g.Np; q0 += Qn)                                                               \
       hipLaunchKernelGGL(kfn, grid, dim3(256), lds, s, *bp, g, q0, std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0); \
   } while (0)
-  if (a.dtype == DFK_BF16) {
-    if (a.hd == 32) LAUNCH_B(bf16raw, 32); else LAUNCH_B(bf16raw, 64);
-  } else {
-    if (a.hd == 32) LAUNCH_B(float, 32); else LAUNCH_B(float, 64);
-  }
+  if (a.hd == 32) LAUNCH_B(float, 32); else LAUNCH_B(float, 64);
 #undef LAUNCH_B
+  reduce_drpb(*bp, g, units, s);
   DFK_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int64_t dfk_wattn_bwd_workspace(const dfk_wattn_args* f) {
+  if (!f || !args_ok(*f)) return -1;
+  if (!f->rpb) return 0;
+  const Geo g = make_geo(*f);
+  const int64_t Lal = (g.L + 3) & ~3;
+  if (f->dtype == DFK_BF16) {  // dS^T scratch (bf16) + per-block dRPB rows
+    const DsPlan pl = ds_plan(*f, g);
+    return ((pl.ds_elems * 2 + 15) & ~15L) + pl.rows * Lal * 4;
+  }
+  return (int64_t)f->B * g.nW * f->heads * Lal * 4;  // fp32: one dRPB row per window-head
 }

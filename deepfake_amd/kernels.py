@@ -173,6 +173,13 @@ def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None
         ba.dpad_q, ba.dpad_k, ba.dpad_v = (p.data_ptr() for p in dpads)
     ba.ld_dqkv = int(ld_dqkv)
     ba.ld_dout = int(dout.stride(0))
+    ws = None
+    if drpb is not None:
+        nbytes = L.lib().dfk_wattn_bwd_workspace(ba.f)
+        if nbytes < 0:
+            raise RuntimeError("dfk_wattn_bwd_workspace: invalid arguments")
+        ws = torch.empty(max(nbytes // 4, 1), device=dout.device, dtype=torch.float32)
+        ba.ws = ws.data_ptr()
     L.check(L.lib().dfk_wattn_bwd(ba, L.stream()), "wattn_bwd")
 
 

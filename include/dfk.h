@@ -127,7 +127,10 @@ int dfk_wattn_fwd(const dfk_wattn_args* a, hipStream_t stream);
  * f.lse its log-sum-exp).  dq/dk/dv are written (=) at the q/k/v layout with
  * row stride ld_dqkv; drpb [L,nH] fp32 (+=); gradients of padded positions
  * (which read the qkv bias in the forward) are summed into dpad_q/k/v
- * [heads*hd] fp32 (+=, may be NULL when the volume needs no padding). */
+ * [heads*hd] fp32 (+=, may be NULL when the volume needs no padding).
+ * ws: fp32 scratch of dfk_wattn_bwd_workspace(&f) bytes for the per-window
+ * dRPB partials (reduced deterministically by a second kernel; NULL falls back
+ * to device-scope atomics on the [L,nH] table, which contend heavily). */
 typedef struct {
   dfk_wattn_args f;
   const void* dout;
@@ -135,8 +138,10 @@ typedef struct {
   float* drpb;
   float* dpad_q; float* dpad_k; float* dpad_v;
   int64_t ld_dqkv, ld_dout;
+  float* ws;
 } dfk_wattn_bwd_args;
 int dfk_wattn_bwd(const dfk_wattn_bwd_args* a, hipStream_t stream);
+int64_t dfk_wattn_bwd_workspace(const dfk_wattn_args* f);
 
 /* Patch im2col for Conv3d/Conv2d with kernel == stride (PatchEmbed3D,
  * video_swin_transformer.py:436,446-453; SwinV2 PatchEmbed swin_transformer2d.py:461,477):

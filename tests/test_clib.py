@@ -12,7 +12,7 @@ HEADER = os.path.join(ROOT, "include", "dfk.h")
 
 def header_symbols():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^int\s+(dfk_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t)\s+(dfk_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_header_matches_binding_table():
