@@ -29,7 +29,7 @@ class GemmArgs(C.Structure):
                 ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("dtype", C.c_int32),
                 ("a_kmajor", C.c_int32), ("b_kmajor", C.c_int32), ("c_f32", C.c_int32), ("nz0", C.c_int32),
                 ("nz1", C.c_int32), ("splitk", C.c_int32), ("act", C.c_int32), ("atomic", C.c_int32),
-                ("beta", C.c_float)]
+                ("beta", C.c_float), ("ws", C.c_void_p)]
 
 
 class WattnArgs(C.Structure):
@@ -61,6 +61,7 @@ class Im2colArgs(C.Structure):
 _VP, _I64, _I32, _F = C.c_void_p, C.c_int64, C.c_int32, C.c_float
 SIGNATURES = {
     "dfk_gemm": [C.POINTER(GemmArgs), _VP],
+    "dfk_gemm_workspace": [C.POINTER(GemmArgs)],
     "dfk_colsum": [_VP, C.c_int, _I64, _I64, _I64, _VP, _VP],
     "dfk_layernorm_fwd": [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, _F, C.c_int, _VP],
     "dfk_layernorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, C.c_int, C.c_int, _VP],
@@ -80,7 +81,7 @@ SIGNATURES = {
 }
 
 _lib = None
-RESTYPES = {"dfk_wattn_bwd_workspace": _I64}
+RESTYPES = {"dfk_wattn_bwd_workspace": _I64, "dfk_gemm_workspace": _I64}
 
 
 def lib():

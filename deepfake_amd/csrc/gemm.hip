@@ -142,8 +142,56 @@ __device__ __forceinline__ float frag_f32(const float* lds, int r0, int kb, int 
   else return lds[(kb + (lane >> 4)) * TL::STRIDE + r0 + (lane & 15)];
 }
 
+// Epilogue for 8 consecutive columns col0.. of output row `row` (batch z0, z1), fp32 sums in v:
+// +bias; act 1: aux <- v, v = gelu(v); act 2: v *= gelu'(aux); +residual; store (beta: += beta*C_old).
+template <typename T>
+__device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1, int row, int col0, float (&v)[8],
+                                          int evec) {
+  const T* bias = g.bias ? reinterpret_cast<const T*>(g.bias) + z1 * g.bias_bs1 : nullptr;
+  const T* res = g.residual ? reinterpret_cast<const T*>(g.residual) + z0 * g.rbs0 + z1 * g.rbs1 : nullptr;
+  const long coff = z0 * g.cbs0 + z1 * g.cbs1;
+  T* aux = g.aux ? reinterpret_cast<T*>(g.aux) + coff : nullptr;
+  const bool full = evec && col0 + 8 <= g.N;
+  const int ncol = min(8, g.N - col0);
+  if (bias) {
+    if (full) { float b8[8]; ld8<T>(bias + col0, b8); for (int e = 0; e < 8; ++e) v[e] += b8[e]; }
+    else for (int e = 0; e < ncol; ++e) v[e] += ldf<T>(bias + col0 + e);
+  }
+  if (g.act == 1) {
+    T* ap = aux ? aux + (long)row * g.ldaux + col0 : nullptr;
+    if (ap) { if (full) st8<T>(ap, v); else for (int e = 0; e < ncol; ++e) stf<T>(ap + e, v[e]); }
+    for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+  } else if (g.act == 2) {
+    const T* ap = aux + (long)row * g.ldaux + col0;
+    float a8[8];
+    if (full) ld8<T>(ap, a8); else for (int e = 0; e < ncol; ++e) a8[e] = ldf<T>(ap + e);
+    for (int e = 0; e < 8; ++e) v[e] *= dgelu_f(a8[e]);
+  }
+  if (res) {
+    const T* rp = res + (long)row * g.ldr + col0;
+    if (full) { float r8[8]; ld8<T>(rp, r8); for (int e = 0; e < 8; ++e) v[e] += r8[e]; }
+    else for (int e = 0; e < ncol; ++e) v[e] += ldf<T>(rp + e);
+  }
+  const long ci = coff + (long)row * g.ldc + col0;
+  if (g.atomic) {
+    float* C = reinterpret_cast<float*>(g.c) + ci;
+    for (int e = 0; e < ncol; ++e) atomicAdd(C + e, v[e]);
+  } else if (g.c_f32) {
+    float* C = reinterpret_cast<float*>(g.c) + ci;
+    for (int e = 0; e < ncol; ++e) C[e] = g.beta != 0.f ? v[e] + g.beta * C[e] : v[e];
+  } else {
+    T* C = reinterpret_cast<T*>(g.c) + ci;
+    if (g.beta != 0.f) {
+      if (full) { float c8v[8]; ld8<T>(C, c8v); for (int e = 0; e < 8; ++e) v[e] += g.beta * c8v[e]; }
+      else for (int e = 0; e < ncol; ++e) v[e] += g.beta * ldf<T>(C + e);
+    }
+    if (full) st8<T>(C, v);
+    else for (int e = 0; e < ncol; ++e) stf<T>(C + e, v[e]);
+  }
+}
+
 template <typename T, bool AK, bool BKM, bool VECOK, bool CONV>
-__global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int evec) {
+__global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int evec, float* slab) {
   using TA = Tile<T, AK, BM>;
   using TB = Tile<T, BKM, BN>;
   constexpr int TBK = GT<T>::BK;
@@ -248,6 +296,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
   const T* res = g.residual ? reinterpret_cast<const T*>(g.residual) + z0 * g.rbs0 + z1 * g.rbs1 : nullptr;
   const long coff = z0 * g.cbs0 + z1 * g.cbs1;
   T* aux = g.aux ? reinterpret_cast<T*>(g.aux) + coff : nullptr;
+  if (slab) {
+    // split-K partial: raw fp32 sums to this split's slab, one row per wave instruction
+    const int col = bn + wn * 64 + lane;
+    float* S = slab + ((long)(z * g.splitk + split) * g.M) * g.N;
+#pragma unroll 4
+    for (int rl = 0; rl < 64; ++rl) {
+      const int row = bm + wm * 64 + rl;
+      if (row < g.M && col < g.N) S[(long)row * g.N + col] = es[rl * ES + lane];
+    }
+    return;
+  }
   if (g.atomic || g.c_f32) {
     // fp32 output (weight gradients): one row per wave instruction = 256 contiguous bytes
     const int col = bn + wn * 64 + lane;
@@ -275,44 +334,36 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
     float v[8];
     *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(es + rl * ES + c8);
     *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(es + rl * ES + c8 + 4);
-    const bool full = evec && col0 + 8 <= g.N;
-    const int ncol = min(8, g.N - col0);
-    if (bias) {
-      if (full) { float b8[8]; ld8<T>(bias + col0, b8); for (int e = 0; e < 8; ++e) v[e] += b8[e]; }
-      else for (int e = 0; e < ncol; ++e) v[e] += ldf<T>(bias + col0 + e);
-    }
-    if (g.act == 1) {
-      T* ap = aux ? aux + (long)row * g.ldaux + col0 : nullptr;
-      if (ap) { if (full) st8<T>(ap, v); else for (int e = 0; e < ncol; ++e) stf<T>(ap + e, v[e]); }
-      for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
-    } else if (g.act == 2) {
-      const T* ap = aux + (long)row * g.ldaux + col0;
-      float a8[8];
-      if (full) ld8<T>(ap, a8); else for (int e = 0; e < ncol; ++e) a8[e] = ldf<T>(ap + e);
-      for (int e = 0; e < 8; ++e) v[e] *= dgelu_f(a8[e]);
-    }
-    if (res) {
-      const T* rp = res + (long)row * g.ldr + col0;
-      if (full) { float r8[8]; ld8<T>(rp, r8); for (int e = 0; e < 8; ++e) v[e] += r8[e]; }
-      else for (int e = 0; e < ncol; ++e) v[e] += ldf<T>(rp + e);
-    }
-    const long ci = coff + (long)row * g.ldc + col0;
-    if (g.atomic) {
-      float* C = reinterpret_cast<float*>(g.c) + ci;
-      for (int e = 0; e < ncol; ++e) atomicAdd(C + e, v[e]);
-    } else if (g.c_f32) {
-      float* C = reinterpret_cast<float*>(g.c) + ci;
-      for (int e = 0; e < ncol; ++e) C[e] = g.beta != 0.f ? v[e] + g.beta * C[e] : v[e];
+    epilogue8<T>(g, z0, z1, row, col0, v, evec);
+  }
+}
+
+// split-K slabs [z][split][M][N] fp32 -> sum -> epilogue (8 columns per thread)
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const dfk_gemm_args g, const float* __restrict__ slab,
+                                                            int splitk, int evec) {
+  const int cg = (g.N + 7) / 8;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long per_z = (long)g.M * cg;
+  const int z = (int)(idx / per_z);
+  if (z >= g.nz0 * g.nz1) return;
+  const long rem = idx - (long)z * per_z;
+  const int row = (int)(rem / cg), col0 = (int)(rem % cg) * 8;
+  const long MN = (long)g.M * g.N;
+  const float* src = slab + (long)z * splitk * MN + (long)row * g.N + col0;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int ncol = min(8, g.N - col0);
+  const bool vec = (g.N % 4) == 0 && ncol == 8;
+  for (int sidx = 0; sidx < splitk; ++sidx, src += MN) {
+    if (vec) {
+      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+      v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
+      v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
     } else {
-      T* C = reinterpret_cast<T*>(g.c) + ci;
-      if (g.beta != 0.f) {
-        if (full) { float c8v[8]; ld8<T>(C, c8v); for (int e = 0; e < 8; ++e) v[e] += g.beta * c8v[e]; }
-        else for (int e = 0; e < ncol; ++e) v[e] += g.beta * ldf<T>(C + e);
-      }
-      if (full) st8<T>(C, v);
-      else for (int e = 0; e < ncol; ++e) stf<T>(C + e, v[e]);
+      for (int e = 0; e < ncol; ++e) v[e] += src[e];
     }
   }
+  epilogue8<T>(g, z / g.nz1, z % g.nz1, row, col0, v, evec);
 }
 
 template <typename T>
@@ -334,14 +385,26 @@ bool view_vec(const dfk_view& v, int vec) {
 }
 
 template <typename T, bool VECOK, bool CONV>
-void dispatch(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, hipStream_t s) {
+void dispatch(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
   if (g.a_kmajor) {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, true, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec);
-    else hipLaunchKernelGGL((gemm_kernel<T, true, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec);
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, true, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_kernel<T, true, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
   } else {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, false, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec);
-    else hipLaunchKernelGGL((gemm_kernel<T, false, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec);
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, false, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_kernel<T, false, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
   }
+}
+
+// automatic K split for grids that cannot fill the chip (caller asked for no split, no atomics)
+template <typename T>
+int auto_splitk(const dfk_gemm_args& g) {
+  constexpr int TBK = GT<T>::BK;
+  if (g.atomic || g.splitk != 1 || g.M <= 0 || g.N <= 0) return 1;
+  const long tiles = (long)dfk_cdiv(g.N, BN) * dfk_cdiv(g.M, BM) * g.nz0 * g.nz1;
+  if (tiles >= 384) return 1;
+  const int maxs = g.K / (2 * TBK);                 // at least two k-tiles per split
+  const int want = (int)dfk_cdiv(768, tiles);
+  return std::max(1, std::min(maxs, want));
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -356,9 +419,12 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   if (g.atomic && (!g.c_f32 || g.bias || g.residual || g.act)) return DFK_EINVAL;
   if (g.act && g.act != 1 && !g.aux) return DFK_EINVAL;
   if (g.M <= 0 || g.N <= 0) return 0;
-  int kchunk = dfk_cdiv(g.K, g.splitk);
+  const int autos = g.ws ? auto_splitk<T>(g) : 1;
+  dfk_gemm_args gg = g;
+  if (autos > 1) gg.splitk = autos;
+  int kchunk = dfk_cdiv(g.K, gg.splitk);
   kchunk = dfk_cdiv(kchunk, TBK) * TBK;
-  dim3 grid(dfk_cdiv(g.N, BN), dfk_cdiv(g.M, BM), g.nz0 * g.nz1 * g.splitk);
+  dim3 grid(dfk_cdiv(g.N, BN), dfk_cdiv(g.M, BM), g.nz0 * g.nz1 * gg.splitk);
   if (grid.y > 65535 || grid.z > 65535) return DFK_EINVAL;
   // vector path also needs the contiguous extents to be whole vectors (else tails load element-wise)
   const bool vec = view_vec(g.a, VEC) && view_vec(g.b, VEC) && (g.a_kmajor ? g.M : g.K) % VEC == 0 &&
@@ -369,11 +435,17 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
                     (!g.residual || (aligned16(g.residual) && g.ldr % 8 == 0 && g.rbs0 % 8 == 0 && g.rbs1 % 8 == 0)) &&
                     (!g.aux || (aligned16(g.aux) && g.ldaux % 8 == 0));
   const bool conv = g.a.conv_cg > 0 || g.b.conv_cg > 0;
+  float* slab = autos > 1 ? reinterpret_cast<float*>(g.ws) : nullptr;
   if (vec) {
-    if (conv) dispatch<T, true, true>(g, grid, kchunk, evec, s);
-    else dispatch<T, true, false>(g, grid, kchunk, evec, s);
+    if (conv) dispatch<T, true, true>(gg, grid, kchunk, evec, slab, s);
+    else dispatch<T, true, false>(gg, grid, kchunk, evec, slab, s);
   } else {
-    dispatch<T, false, true>(g, grid, kchunk, evec, s);
+    dispatch<T, false, true>(gg, grid, kchunk, evec, slab, s);
+  }
+  if (slab) {
+    const long threads = (long)g.nz0 * g.nz1 * g.M * dfk_cdiv(g.N, 8);
+    hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3((unsigned)dfk_cdiv(threads, 256)), dim3(256), 0, s, g, slab,
+                       autos, evec ? 1 : 0);
   }
   DFK_CHECK_LAUNCH();
   return 0;
@@ -384,6 +456,13 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
 extern "C" int dfk_gemm(const dfk_gemm_args* g, hipStream_t s) {
   if (!g) return DFK_EINVAL;
   return g->dtype == DFK_BF16 ? launch<bf16raw>(*g, s) : launch<float>(*g, s);
+}
+
+extern "C" int64_t dfk_gemm_workspace(const dfk_gemm_args* g) {
+  if (!g) return -1;
+  const int autos = g->dtype == DFK_BF16 ? auto_splitk<bf16raw>(*g) : auto_splitk<float>(*g);
+  if (autos <= 1) return 0;
+  return (int64_t)autos * g->nz0 * g->nz1 * g->M * g->N * 4;
 }
 
 extern "C" int dfk_colsum(const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld, float* out,

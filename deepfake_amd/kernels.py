@@ -49,6 +49,11 @@ def gemm(a, a_ld, a_kmajor, b, b_ld, b_kmajor, M, N, K, c, ldc, *, dtype, c_f32=
     for t in (a, b, c):
         if not t.is_cuda:
             raise RuntimeError("deepfake_amd: tensors must be on the HIP device (no CPU fallback)")
+    ws = None
+    nbytes = L.lib().dfk_gemm_workspace(g)
+    if nbytes > 0:
+        ws = torch.empty(nbytes // 4, device=c.device, dtype=torch.float32)
+        g.ws = ws.data_ptr()
     L.check(L.lib().dfk_gemm(g, L.stream()), f"gemm M={M} N={N} K={K}")
 
 

@@ -73,8 +73,13 @@ typedef struct {
   int32_t act;
   int32_t atomic;
   float beta;
+  void* ws;             /* fp32 split-K slabs, dfk_gemm_workspace(g) bytes (NULL: no automatic split) */
 } dfk_gemm_args;
 int dfk_gemm(const dfk_gemm_args* g, hipStream_t stream);
+/* Bytes of scratch dfk_gemm wants in g->ws: grids too small to fill the chip (the
+ * wav2vec2 / SwinV2-stage-3 Linears, M ~ 1.6k rows) are split along K into fp32
+ * slabs that a second kernel sums before the epilogue.  0 = no split. */
+int64_t dfk_gemm_workspace(const dfk_gemm_args* g);
 
 /* out[j] (+)= sum_i x[i*ld + j] (fp32 atomics).  Linear bias gradients. */
 int dfk_colsum(const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld, float* out, hipStream_t stream);

@@ -15,7 +15,8 @@ SHAPES = [  # (name, M tokens, N out, K in)
     ("vst1.proj", 401408, 96, 96), ("vst2.fc1", 100352, 768, 192), ("vst3.fc1", 25088, 1536, 384),
     ("vst3.fc2", 25088, 384, 1536), ("vst4.fc1", 6272, 3072, 768), ("mel1.fc1", 25088, 512, 128),
     ("mel3.fc1", 1568, 2048, 512), ("w2v.qkv", 1592, 2304, 768), ("w2v.fc1", 1592, 3072, 768),
-    ("w2v.fc2", 1592, 768, 3072), ("merge1", 100352, 192, 384),
+    ("w2v.fc2", 1592, 768, 3072), ("merge1", 100352, 192, 384), ("mel3.proj", 1568, 512, 512),
+    ("mel3.fc2", 1568, 512, 2048), ("w2v.proj", 1592, 768, 768),
 ]
 
 
@@ -34,6 +35,7 @@ def t(fn, it=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--torch", action="store_true", help="also time torch (hipBLASLt) for reference")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     tot = {"fwd": 0.0, "dx": 0.0, "dw": 0.0}
@@ -53,7 +55,14 @@ def main():
         tot["dw"] += tw
         bytes_f = (M * Kd + M * N + N * Kd) * x.element_size()
         print(f"{name:10s} M={M:7d} N={N:5d} K={Kd:5d}  fwd {fl / tf / 1e12:7.1f} TF ({bytes_f / tf / 1e9:6.0f} GB/s)"
-              f"  dx {fl / tx / 1e12:7.1f} TF  dw {fl / tw / 1e12:7.1f} TF   [{tf * 1e6:.0f}/{tx * 1e6:.0f}/{tw * 1e6:.0f} us]")
+              f"  dx {fl / tx / 1e12:7.1f} TF  dw {fl / tw / 1e12:7.1f} TF   [{tf * 1e6:.0f}/{tx * 1e6:.0f}/{tw * 1e6:.0f} us]",
+              flush=True)
+        if a.torch:
+            rf = t(lambda: torch.nn.functional.linear(x, w))
+            rx = t(lambda: dy @ w)
+            rw = t(lambda: dy.t() @ x)
+            print(f"{'  torch':10s} {'':33s}  fwd {fl / rf / 1e12:7.1f} TF {'':13s}  dx {fl / rx / 1e12:7.1f} TF  "
+                  f"dw {fl / rw / 1e12:7.1f} TF   [{rf * 1e6:.0f}/{rx * 1e6:.0f}/{rw * 1e6:.0f} us]", flush=True)
     print("total us", {k: round(v * 1e6) for k, v in tot.items()})
 
 
