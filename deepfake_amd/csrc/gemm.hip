@@ -51,11 +51,17 @@ template <typename T, bool VECOK, bool CONV>
 __device__ __forceinline__ uint4 view_load(const T* base, const dfk_view& v, long r, long c, bool rok, long climit) {
   constexpr int VEC = 16 / sizeof(T);
   uint4 z = make_uint4(0, 0, 0, 0);
-  if (!rok || c >= climit) return z;
   if constexpr (VECOK) {
+    // branch-free: an out-of-range element loads from the view base and is masked to zero, so the
+    // compiler keeps every tile load in flight (a branch around a load makes it wait vmcnt(0) there)
     const long o = view_off<CONV>(v, r, c);
-    return o < 0 ? z : *reinterpret_cast<const uint4*>(base + o);
+    const bool ok = rok && c < climit && o >= 0;
+    uint4 x = *reinterpret_cast<const uint4*>(base + (ok ? o : 0));
+    const uint32_t m = ok ? 0xffffffffu : 0u;
+    x.x &= m; x.y &= m; x.z &= m; x.w &= m;
+    return x;
   } else {
+    if (!rok || c >= climit) return z;
     uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
