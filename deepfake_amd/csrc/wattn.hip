@@ -67,6 +67,35 @@ __device__ __forceinline__ uint4 ld16(const T* p) {
   return p ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
 }
 
+// Branch-free token loads: the address is always valid (invalid tokens read the buffer base) and the
+// value is masked afterwards, so no branch (and no vmcnt(0) wait inside it) surrounds the load.
+template <typename T>
+__device__ __forceinline__ const T* tok_src(const void* base, const void* pad, int row, long ld, int off, bool& ok) {
+  const bool real = row >= 0, padded = row == -1 && pad != nullptr;
+  ok = real || padded;
+  const T* pr = reinterpret_cast<const T*>(base) + (real ? (long)row * ld + off : 0);
+  const T* pp = reinterpret_cast<const T*>(padded ? pad : base) + (padded ? off : 0);
+  return real ? pr : pp;
+}
+
+template <typename T>
+__device__ __forceinline__ uint4 tok_ld16(const void* base, const void* pad, int row, long ld, int off) {
+  bool ok;
+  const T* p = tok_src<T>(base, pad, row, ld, off, ok);
+  uint4 x = *reinterpret_cast<const uint4*>(p);
+  const uint32_t m = ok ? 0xffffffffu : 0u;
+  x.x &= m; x.y &= m; x.z &= m; x.w &= m;
+  return x;
+}
+
+template <typename T>
+__device__ __forceinline__ T tok_ld1(const void* base, const void* pad, int row, long ld, int off) {
+  bool ok;
+  const T* p = tok_src<T>(base, pad, row, ld, off, ok);
+  const T x = *p;
+  return ok ? x : (T)0;
+}
+
 // ---------------------------------------------------------------- forward
 template <typename T, int HD>
 __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, const Geo g, int qsplit) {
@@ -97,8 +126,8 @@ __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, 
   for (int idx = tid; idx < g.Np * (HD / VEC); idx += 256) {
     const int i = idx / (HD / VEC), c = (idx % (HD / VEC)) * VEC;
     const TokInfo t = tok[i];
-    const uint4 kv = ld16<T>(tok_ptr<T>(a.k, a.pad_k, t.row, a.ld_qkv, hoff + c));
-    const uint4 vv = ld16<T>(tok_ptr<T>(a.v, a.pad_v, t.row, a.ld_qkv, hoff + c));
+    const uint4 kv = tok_ld16<T>(a.k, a.pad_k, t.row, a.ld_qkv, hoff + c);
+    const uint4 vv = tok_ld16<T>(a.v, a.pad_v, t.row, a.ld_qkv, hoff + c);
     *reinterpret_cast<uint4*>(Ks + i * HD + c) = kv;
     if constexpr (BF) {
       const bf16raw* e = reinterpret_cast<const bf16raw*>(&vv);
@@ -127,7 +156,7 @@ __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, 
       bf16x8 qf[HD / 32];
 #pragma unroll
       for (int es = 0; es < HD / 32; ++es) {
-        uint4 u = qp ? *reinterpret_cast<const uint4*>(qp + es * 32 + grp * 8) : make_uint4(0, 0, 0, 0);
+        uint4 u = tok_ld16<T>(a.q, a.pad_q, tq.row, a.ld_qkv, hoff + es * 32 + grp * 8);
         qf[es] = *reinterpret_cast<bf16x8*>(&u);
       }
       for (int kb = 0; kb < nkb; ++kb) {
@@ -737,15 +766,11 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
     if (idx < Qn * CH) {
       const int li = idx / CH, c = (idx % CH) * 8;
       const int row = trow[q0 + li];
-      const bf16raw* qp = row >= 0 ? qg + (long)row * a.ld_qkv + hoff + c
-                                   : (row == -1 && a.pad_q ? reinterpret_cast<const bf16raw*>(a.pad_q) + hoff + c
-                                                           : nullptr);
-      uint4 dv = make_uint4(0, 0, 0, 0);
-      if (row >= 0) {
-        dv = *reinterpret_cast<const uint4*>(dog + (long)row * ba.ld_dout + hoff + c);
-        d = dot8_bf16(*reinterpret_cast<const uint4*>(og + (long)row * a.ld_out + hoff + c), dv);
-      }
-      *reinterpret_cast<uint4*>(Qs + swz<HD>(li, c)) = ld16<bf16raw>(qp);
+      const uint4 qv = tok_ld16<bf16raw>(a.q, a.pad_q, row, a.ld_qkv, hoff + c);
+      const uint4 dv = tok_ld16<bf16raw>(ba.dout, nullptr, row, ba.ld_dout, hoff + c);
+      const uint4 ov = tok_ld16<bf16raw>(a.out, nullptr, row, a.ld_out, hoff + c);
+      d = dot8_bf16(ov, dv);
+      *reinterpret_cast<uint4*>(Qs + swz<HD>(li, c)) = qv;
       *reinterpret_cast<uint4*>(dOs + swz<HD>(li, c)) = dv;
     }
 #pragma unroll
@@ -777,14 +802,10 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
       const int row = trow[k];
       kpk[h2] = tpk[k];
       kneg[h2] = row == -2 ? -INFINITY : 0.f;
-      const bf16raw* kp = tok_ptr<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff);
-      const bf16raw* vp = tok_ptr<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff);
 #pragma unroll
       for (int es = 0; es < HD / 32; ++es) {
-        uint4 u = kp ? *reinterpret_cast<const uint4*>(kp + es * 32 + grp * 8) : make_uint4(0, 0, 0, 0);
-        kB[h2][es] = __builtin_bit_cast(bf16x8, u);
-        u = vp ? *reinterpret_cast<const uint4*>(vp + es * 32 + grp * 8) : make_uint4(0, 0, 0, 0);
-        vB[h2][es] = __builtin_bit_cast(bf16x8, u);
+        kB[h2][es] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + es * 32 + grp * 8));
+        vB[h2][es] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + es * 32 + grp * 8));
       }
 #pragma unroll
       for (int et = 0; et < HD / 16; ++et) { dK[h2][et] = f32x4{0, 0, 0, 0}; dV[h2][et] = f32x4{0, 0, 0, 0}; }
@@ -792,9 +813,9 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int row = trow[kbc * 32 + grp * 8 + j];
-      const bf16raw* kp = tok_ptr<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + ql);
 #pragma unroll
-      for (int et = 0; et < HD / 16; ++et) kN[et][j] = kp ? __builtin_bit_cast(__bf16, kp[et * 16]) : (__bf16)0.f;
+      for (int et = 0; et < HD / 16; ++et)
+        kN[et][j] = __builtin_bit_cast(__bf16, tok_ld1<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + ql + et * 16));
     }
 
     for (int qb = 0; qb < nqb; ++qb) {
