@@ -29,7 +29,7 @@ class GemmArgs(C.Structure):
                 ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("dtype", C.c_int32),
                 ("a_kmajor", C.c_int32), ("b_kmajor", C.c_int32), ("c_f32", C.c_int32), ("nz0", C.c_int32),
                 ("nz1", C.c_int32), ("splitk", C.c_int32), ("act", C.c_int32), ("atomic", C.c_int32),
-                ("beta", C.c_float), ("ws", C.c_void_p)]
+                ("beta", C.c_float), ("ws", C.c_void_p), ("rowsum", C.c_void_p)]
 
 
 class WattnArgs(C.Structure):

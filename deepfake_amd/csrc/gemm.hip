@@ -196,7 +196,7 @@ __device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1
   }
 }
 
-template <typename T, bool AK, bool BKM, bool VECOK, bool CONV>
+template <typename T, bool AK, bool BKM, bool VECOK, bool CONV, bool RS = false>
 __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int evec, float* slab) {
   using TA = Tile<T, AK, BM>;
   using TB = Tile<T, BKM, BN>;
@@ -232,6 +232,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused row sums of A (bias gradients): one wave column of the first N-tile multiplies A by ones
+  const bool do_rs = RS && tn == 0 && wn == 0;   // RS: instantiated only for the dW (k-major x k-major) GEMM
+  f32x4 accr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) accr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[4], rb[4];
   if (kbeg < kend) {
@@ -263,6 +268,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
 #pragma unroll
           for (int ni = 0; ni < 4; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+        if (RS && do_rs) {
+          bf16x8 ones;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) accr[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], ones, accr[mi], 0, 0, 0);
+        }
       }
     } else {
 #pragma unroll
@@ -277,6 +289,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
 #pragma unroll
           for (int ni = 0; ni < 4; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+        if (RS && do_rs)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi) accr[mi] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi], 1.0f, accr[mi], 0, 0, 0);
       }
     }
     if (more) {
@@ -287,6 +302,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
     cur ^= 1;
   }
 
+  if (RS && do_rs && (lane & 15) == 0) {   // every column of A*ones is the row sum: lanes of column 0 publish it
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = bm + wm * 64 + mi * 16 + (lane >> 4) * 4 + r;
+        if (row < g.M) atomicAdd(g.rowsum + row, accr[mi][r]);
+      }
+  }
   // ---- epilogue: stage each wave's 64x64 fp32 tile through LDS (the 16x16 MFMA C/D
   // layout is col = lane&15, row = (lane>>4)*4 + r), then every lane owns 8
   // consecutive columns of a row: 16-B loads of bias/residual/aux and 16-B stores.
@@ -393,7 +417,10 @@ bool view_vec(const dfk_view& v, int vec) {
 template <typename T, bool VECOK, bool CONV>
 void dispatch(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
   if (g.a_kmajor) {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, true, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    if (g.b_kmajor) {
+      if (g.rowsum) hipLaunchKernelGGL((gemm_kernel<T, true, true, VECOK, CONV, true>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+      else hipLaunchKernelGGL((gemm_kernel<T, true, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    }
     else hipLaunchKernelGGL((gemm_kernel<T, true, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
   } else {
     if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, false, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
@@ -424,6 +451,7 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   if (g.splitk > 1 && !g.atomic) return DFK_EINVAL;
   if (g.atomic && (!g.c_f32 || g.bias || g.residual || g.act)) return DFK_EINVAL;
   if (g.act && g.act != 1 && !g.aux) return DFK_EINVAL;
+  if (g.rowsum && (g.nz0 != 1 || g.nz1 != 1 || !g.a_kmajor || !g.b_kmajor)) return DFK_EINVAL;
   if (g.M <= 0 || g.N <= 0) return 0;
   const int autos = g.ws ? auto_splitk<T>(g) : 1;
   dfk_gemm_args gg = g;

@@ -88,13 +88,14 @@ class LinearFn(torch.autograd.Function):
         dz = K.gelu_bwd(dy, aux) if ctx.act == 1 else dy
         w = compute_weight(weight, x.dtype)
         dx = K.linear_dx(dz, w) if ctx.needs_input_grad[0] else None
-        dw = None
+        dw = db = None
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            dw = K.linear_dw(dz, x, grad_sink(weight))
-            dw = grad_done(weight, dw)
-        db = None
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = grad_sink(bias) if want_b else None      # bias gradient fused into the dW pass
+            dw = grad_done(weight, K.linear_dw(dz, x, grad_sink(weight), db=db))
+        elif want_b:
             db = K.colsum(dz, grad_sink(bias))
+        if want_b:
             db = grad_done(bias, db)
         return dx, dw, db, None, (dy if ctx.has_res else None)
 
@@ -129,11 +130,13 @@ class MlpFn(torch.autograd.Function):
         dy = dy.contiguous()
         dt = x.dtype
         dpre = K.linear_dx(dy, compute_weight(w2, dt), act=2, aux=pre)      # (dy W2) * gelu'(pre)
-        dw2 = grad_done(w2, K.linear_dw(dy, h, grad_sink(w2)))
-        db2 = grad_done(b2, K.colsum(dy, grad_sink(b2)))
+        db2 = grad_sink(b2)
+        dw2 = grad_done(w2, K.linear_dw(dy, h, grad_sink(w2), db=db2))
+        db2 = grad_done(b2, db2)
         dx = K.linear_dx(dpre, compute_weight(w1, dt)) if ctx.needs_input_grad[0] else None
-        dw1 = grad_done(w1, K.linear_dw(dpre, x, grad_sink(w1)))
-        db1 = grad_done(b1, K.colsum(dpre, grad_sink(b1)))
+        db1 = grad_sink(b1)
+        dw1 = grad_done(w1, K.linear_dw(dpre, x, grad_sink(w1), db=db1))
+        db1 = grad_done(b1, db1)
         return dx, dw1, db1, dw2, db2, (dy if ctx.has_res else None)
 
 
@@ -401,7 +404,6 @@ class PatchEmbedFn(torch.autograd.Function):
     def backward(ctx, dy):
         cols, weight, bias = ctx.saved_tensors
         dy = dy.contiguous()
-        dw = grad_sink(weight)
-        K.linear_dw(dy, cols, dw.view(weight.shape[0], -1))
-        db = grad_done(bias, K.colsum(dy, grad_sink(bias)))
-        return None, grad_done(weight, dw), db, None, None, None
+        dw, db = grad_sink(weight), grad_sink(bias)
+        K.linear_dw(dy, cols, dw.view(weight.shape[0], -1), db=db)
+        return None, grad_done(weight, dw), grad_done(bias, db), None, None, None

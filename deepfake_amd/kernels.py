@@ -24,7 +24,8 @@ def _view(t, ld, bs0=0, bs1=0, conv=None):
 
 def gemm(a, a_ld, a_kmajor, b, b_ld, b_kmajor, M, N, K, c, ldc, *, dtype, c_f32=False, bias=None,
          residual=None, ldr=0, aux=None, ldaux=0, act=0, beta=0.0, atomic=False, splitk=1,
-         nz=(1, 1), a_bs=(0, 0), b_bs=(0, 0), c_bs=(0, 0), r_bs=(0, 0), a_conv=None, b_conv=None, bias_bs1=0):
+         nz=(1, 1), a_bs=(0, 0), b_bs=(0, 0), c_bs=(0, 0), r_bs=(0, 0), a_conv=None, b_conv=None, bias_bs1=0,
+         rowsum=None):
     """Raw dfk_gemm.  a/b/c are tensors (base pointers); see include/dfk.h."""
     g = L.GemmArgs()
     g.bias_bs1 = int(bias_bs1)
@@ -46,6 +47,7 @@ def gemm(a, a_ld, a_kmajor, b, b_ld, b_kmajor, M, N, K, c, ldc, *, dtype, c_f32=
     g.act = int(act)
     g.atomic = int(atomic)
     g.beta = float(beta)
+    g.rowsum = rowsum.data_ptr() if rowsum is not None else None
     for t in (a, b, c):
         if not t.is_cuda:
             raise RuntimeError("deepfake_amd: tensors must be on the HIP device (no CPU fallback)")
@@ -84,13 +86,14 @@ def splitk_for(tiles, K, min_k=256):
     return max(1, min(_CU_TARGET_BLOCKS // max(tiles, 1), max(K // min_k, 1)))
 
 
-def linear_dw(dy, x, dw):
-    """dw[N,K] (fp32, +=) += dy[M,N]^T @ x[M,K]  (split over M, fp32 atomics)."""
+def linear_dw(dy, x, dw, db=None):
+    """dw[N,K] (fp32, +=) += dy[M,N]^T @ x[M,K]  (split over M, fp32 atomics); with db [N] fp32:
+    db += column sums of dy (the bias gradient) from the same pass over dy."""
     M, N = dy.shape
     K = x.shape[1]
     tiles = math.ceil(N / 128) * math.ceil(K / 128)
     gemm(dy, dy.stride(0), True, x, x.stride(0), True, N, K, M, dw, dw.stride(0), dtype=L.dt(dy), c_f32=True,
-         atomic=True, splitk=splitk_for(tiles, M))
+         atomic=True, splitk=splitk_for(tiles, M), rowsum=db)
     return dw
 
 

@@ -74,6 +74,8 @@ typedef struct {
   int32_t atomic;
   float beta;
   void* ws;             /* fp32 split-K slabs, dfk_gemm_workspace(g) bytes (NULL: no automatic split) */
+  float* rowsum;        /* optional, nz0 = nz1 = 1: rowsum[i] += sum_k A(i,k) (fp32) — the bias gradient
+                           of a Linear when A = dy^T, computed by one extra MFMA against a ones operand */
 } dfk_gemm_args;
 int dfk_gemm(const dfk_gemm_args* g, hipStream_t stream);
 /* Bytes of scratch dfk_gemm wants in g->ws: grids too small to fill the chip (the
