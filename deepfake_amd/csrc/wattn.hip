@@ -54,6 +54,15 @@ __device__ __forceinline__ TokInfo token_info(const dfk_wattn_args& a, const Geo
   return t;
 }
 
+// only the row of token i (the forward's Q/K/V gathers)
+__device__ __forceinline__ int token_info_row(const dfk_wattn_args& a, const Geo& g, int b, int win, int i) {
+  if (i >= g.N) return -2;
+  const int wwi = win % g.nww, whi = (win / g.nww) % g.nwh, wdi = win / (g.nww * g.nwh);
+  const int td = i / (a.wh * a.ww), th = (i / a.ww) % a.wh, tw = i % a.ww;
+  const int od = (wdi * a.wd + td + a.sd) % g.Dp, oh = (whi * a.wh + th + a.sh) % g.Hp, ow = (wwi * a.ww + tw + a.sw) % g.Wp;
+  return (od < a.D && oh < a.H && ow < a.W) ? ((b * a.D + od) * a.H + oh) * a.W + ow : -1;
+}
+
 // address of element e of head h for token info row (or the pad vector / zero)
 template <typename T>
 __device__ __forceinline__ const T* tok_ptr(const void* base, const void* pad, int row, long ld, int off) {
@@ -94,6 +103,43 @@ __device__ __forceinline__ T tok_ld1(const void* base, const void* pad, int row,
   const T* p = tok_src<T>(base, pad, row, ld, off, ok);
   const T x = *p;
   return ok ? x : (T)0;
+}
+
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v lds_short4;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr int kBwdWaves = 8;
+constexpr int kSdStride = 40;  // bf16 row stride of the per-wave dS^T scratch [32 keys][32 queries]
+
+// element offset of (row, col) in a [rows][HD] bf16 tile with 16-B chunks XOR-swizzled by row:
+// conflict-free 16-B row reads (A operands) and 8-B transposed reads (tr16 B operands)
+template <int HD>
+__device__ __forceinline__ int swz(int row, int col) {
+  const int f = HD == 32 ? ((row & 2) | ((row >> 2) & 1)) : (((row & 3) << 1) | ((row >> 2) & 1));
+  return row * HD + (((col >> 3) ^ f) << 3) + (col & 7);
+}
+
+// fp32 [rows][HD] accumulator: the 4 rows a C fragment touches land in two bank halves
+template <int HD>
+__device__ __forceinline__ int dq_off(int row, int col) {
+  return row * HD + (col ^ (((row >> 2) & 1) << 4));
+}
+
+__device__ __forceinline__ bf16x8 tr16x2(const bf16raw* p0, const bf16raw* p1) {
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(p0));
+  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(p1));
+  short8 u = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+__device__ __forceinline__ float dot8_bf16(uint4 x, uint4 y) {
+  const bf16raw* a = reinterpret_cast<const bf16raw*>(&x);
+  const bf16raw* b = reinterpret_cast<const bf16raw*>(&y);
+  float d = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d += bf2f(a[j]) * bf2f(b[j]);
+  return d;
 }
 
 // ---------------------------------------------------------------- forward
@@ -287,6 +333,198 @@ __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, 
   }
 }
 
+// ------------------------------------------------------------ bf16 forward
+// One workgroup = one (clip, window, head) (x qsplit), 4 waves; K and V of the window staged once in
+// XOR-swizzled LDS tiles.  Each wave owns 32-query blocks: S^T = K Q^T with the query on the lane (row
+// statistics are per-lane scalars, reduced over the 4 lane groups), base-2 online softmax with a lazy
+// rescale (only when some query's running max grows by more than kRescale), O^T += V^T P^T with P^T taken
+// straight from the accumulators and V^T read by ds_read_tr16, and the softmax denominator produced by
+// the same MFMA chain (a ones tile in place of V^T) instead of per-element adds.
+constexpr float kRescale = 8.f;   // log2 units: P stays <= 2^8 between rescales
+
+template <int HD, bool RPB, bool MASK>
+__global__ __launch_bounds__(256) void wattn_fwd_bf16_kernel(const dfk_wattn_args a, const Geo g, int qsplit) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Lal = (g.L + 3) & ~3;
+  char* p = smem;
+  int& mixed = *reinterpret_cast<int*>(p); p += 16;             // window holds more than one shift region
+  int* tpk = reinterpret_cast<int*>(p); p += 4 * g.Np;          // pos << 5 | label; label 31 = beyond N
+  float* rpb2 = reinterpret_cast<float*>(p); p += 4 * Lal;      // rpb * log2(e)
+  bf16raw* Ks = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)g.Np * HD;
+  bf16raw* Vs = reinterpret_cast<bf16raw*>(p);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = lane >> 4, ql = lane & 15, tq = ql >> 2, tp = ql & 3;
+  int unit = blockIdx.x;
+  const int head = unit % a.heads;
+  unit /= a.heads;
+  const int win = unit % g.nW, b = unit / g.nW;
+  const float* mrow = MASK ? a.mask + (((long)b * g.nW + win) % a.mask_nw) * g.N * g.N : nullptr;
+  const int hoff = head * HD;
+  if (tid == 0) mixed = 0;
+  __syncthreads();
+  int lab0 = -1;
+  for (int i = tid; i < g.Np; i += blockDim.x) {
+    const TokInfo t = token_info(a, g, b, win, i);
+    tpk[i] = (t.pos << 5) | (t.row == -2 ? 31 : t.lab);
+    if (t.row != -2) {
+      if (lab0 < 0) lab0 = t.lab;
+      else if (t.lab != lab0) mixed = 1;
+    }
+  }
+  if (g.use_mask && lab0 >= 0 && lab0 != token_info(a, g, b, win, 0).lab) mixed = 1;
+  if (RPB)
+    for (int l = tid; l < g.L; l += blockDim.x) rpb2[l] = a.rpb[(long)l * a.heads + head] * kLog2e;
+  __syncthreads();
+  constexpr int CH = HD / 8;
+  for (int idx = tid; idx < g.Np * CH; idx += blockDim.x) {
+    const int i = idx / CH, c = (idx % CH) * 8;
+    const int row = token_info_row(a, g, b, win, i);
+    *reinterpret_cast<uint4*>(Ks + swz<HD>(i, c)) = tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + c);
+    *reinterpret_cast<uint4*>(Vs + swz<HD>(i, c)) = tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + c);
+  }
+  __syncthreads();
+  const bool use_mask = g.use_mask && mixed;
+
+  const float scale2 = a.scale * kLog2e;
+  const float mpen = -100.f * kLog2e;
+  const int nkb = g.Np / 32, nqb = g.Np / 32;
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+  const int nw = blockDim.x >> 6;
+  for (int qb = blockIdx.y * nw + wave; qb < nqb; qb += nw * qsplit) {
+    // the lane's queries (one per 16-query half) and their Q^T B operands
+    int qpk[2], qrow[2];
+    bf16x8 qf[2][HD / 32];
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const int q = qb * 32 + qh * 16 + ql;
+      qpk[qh] = tpk[q];
+      qrow[qh] = q < g.N ? token_info_row(a, g, b, win, q) : -2;
+#pragma unroll
+      for (int es = 0; es < HD / 32; ++es)
+        qf[qh][es] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.q, a.pad_q, qrow[qh], a.ld_qkv, hoff + es * 32 + grp * 8));
+    }
+    float m[2] = {-INFINITY, -INFINITY};
+    f32x4 o[2][HD / 16], lsum[2];
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      lsum[qh] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et) o[qh][et] = f32x4{0, 0, 0, 0};
+    }
+    for (int kb = 0; kb < nkb; ++kb) {
+      // key statistics of the lane's rows (keys kb*32 + h2*16 + 4grp + r) and the K A-operands
+      int4 kp[2];
+      bf16x8 ka[2][HD / 32];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        kp[h2] = *reinterpret_cast<const int4*>(tpk + kb * 32 + h2 * 16 + grp * 4);
+#pragma unroll
+        for (int es = 0; es < HD / 32; ++es)
+          ka[h2][es] = *reinterpret_cast<const bf16x8*>(Ks + swz<HD>(kb * 32 + h2 * 16 + ql, es * 32 + grp * 8));
+      }
+      float x[2][2][4];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          f32x4 sacc = f32x4{0, 0, 0, 0};
+#pragma unroll
+          for (int es = 0; es < HD / 32; ++es)
+            sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[h2][es], qf[qh][es], sacc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int kpk = kp[h2][r];
+            float v = sacc[r] * scale2;
+            if (RPB) v += rpb2[(qpk[qh] >> 5) - (kpk >> 5) + g.C0];
+            if (use_mask) v += ((qpk[qh] ^ kpk) & 31) ? mpen : 0.f;
+            if constexpr (MASK) {
+              const int q = qb * 32 + qh * 16 + ql, k = kb * 32 + h2 * 16 + grp * 4 + r;
+              if (q < g.N && k < g.N) v += mrow[q * g.N + k] * kLog2e;
+            }
+            x[qh][h2][r] = v;
+          }
+        }
+      if (kb == nkb - 1) {   // keys beyond N (the only padded key block)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if ((kp[h2][r] & 31) == 31)
+#pragma unroll
+              for (int qh = 0; qh < 2; ++qh) x[qh][h2][r] = -INFINITY;
+      }
+      // running max (per query = per lane column, reduced over the 4 lane groups), lazy rescale
+      bool grow = false;
+      float mnew[2];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        float mx = x[qh][0][0];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, x[qh][h2][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mnew[qh] = mx > m[qh] + kRescale ? mx : m[qh];
+        grow |= mnew[qh] != m[qh];
+      }
+      if (__builtin_amdgcn_ballot_w64(grow) != 0) {
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const float alpha = m[qh] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[qh] - mnew[qh]);
+          m[qh] = mnew[qh];
+          lsum[qh] *= alpha;
+#pragma unroll
+          for (int et = 0; et < HD / 16; ++et) o[qh][et] *= alpha;
+        }
+      }
+      // P^T B operands: key slot j <-> (h2 = j>>2, row 4grp + (j&3))
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pf[qh][h2 * 4 + r] = (__bf16)__builtin_amdgcn_exp2f(x[qh][h2][r] - m[qh]);
+      // O^T[e][q] += V^T P^T (V^T by tr16 with the same key permutation); lsum += ones^T P^T
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et) {
+        const int c = et * 16 + tp * 4;
+        const bf16x8 va = tr16x2(Vs + swz<HD>(kb * 32 + grp * 4 + tq, c), Vs + swz<HD>(kb * 32 + 16 + grp * 4 + tq, c));
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) o[qh][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pf[qh], o[qh][et], 0, 0, 0);
+      }
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qh], lsum[qh], 0, 0, 0);
+    }
+    // O = O^T / l: lane holds e = et*16 + 4grp + r of query ql
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const int q = qb * 32 + qh * 16 + ql;
+      const float l = lsum[qh][0];
+      const float inv = 1.f / l;
+      if (qrow[qh] >= 0) {
+        bf16raw* op = reinterpret_cast<bf16raw*>(a.out) + (long)qrow[qh] * a.ld_out + hoff;
+#pragma unroll
+        for (int et = 0; et < HD / 16; ++et) {
+          uint2 u;
+          u.x = (uint32_t)f2bf(o[qh][et][0] * inv) | ((uint32_t)f2bf(o[qh][et][1] * inv) << 16);
+          u.y = (uint32_t)f2bf(o[qh][et][2] * inv) | ((uint32_t)f2bf(o[qh][et][3] * inv) << 16);
+          *reinterpret_cast<uint2*>(op + et * 16 + grp * 4) = u;
+        }
+      }
+      if (a.lse && grp == 0 && q < g.N) a.lse[((long)blockIdx.x) * g.Np + q] = (m[qh] + __log2f(l)) * 0.6931471805599453f;
+    }
+  }
+}
+
+size_t fwd_lds_bf16(const dfk_wattn_args& a, const Geo& g) {
+  return 16 + 4 * (size_t)g.Np + 4 * (size_t)((g.L + 3) & ~3) + 4 * (size_t)g.Np * a.hd;
+}
+
 Geo make_geo(const dfk_wattn_args& a) {
   Geo g;
   g.Dp = dfk_cdiv(a.D, a.wd) * a.wd;
@@ -326,6 +564,36 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
   if (!ap || !args_ok(*ap)) return DFK_EINVAL;
   const dfk_wattn_args& a = *ap;
   const Geo g = make_geo(a);
+  if (a.dtype == DFK_BF16) {
+    const size_t lds = fwd_lds_bf16(a, g);
+    if (lds > 160 * 1024) return DFK_EINVAL;
+    const long units = (long)a.B * g.nW * a.heads;
+    if (units <= 0) return 0;
+    const int nqb = g.Np / 32;
+    const int nw = std::min(4, nqb);   // small windows (SwinV2 7x7: two query blocks) get fewer waves
+    const int qsplit = (int)std::max<long>(1, std::min<long>(dfk_cdiv(nqb, nw), dfk_cdiv(1024, units)));
+    dim3 grid((unsigned)units, qsplit);
+#define LAUNCH_F16(HD, RPB, MASK)                                                                          \
+  do {                                                                                                     \
+    auto kfn = wattn_fwd_bf16_kernel<HD, RPB, MASK>;                                                       \
+    static bool attr_set = false;                                                                          \
+    if (!attr_set) {                                                                                       \
+      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      attr_set = true;                                                                                     \
+    }                                                                                                      \
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), lds, s, a, g, qsplit);                                    \
+  } while (0)
+#define PICK_F16(HD)                                                                            \
+  do {                                                                                          \
+    if (a.rpb) { if (a.mask) LAUNCH_F16(HD, true, true); else LAUNCH_F16(HD, true, false); }   \
+    else { if (a.mask) LAUNCH_F16(HD, false, true); else LAUNCH_F16(HD, false, false); }       \
+  } while (0)
+    if (a.hd == 32) PICK_F16(32); else PICK_F16(64);
+#undef PICK_F16
+#undef LAUNCH_F16
+    DFK_CHECK_LAUNCH();
+    return 0;
+  }
   const size_t lds = fwd_lds(a, g);
   if (lds > 160 * 1024) return DFK_EINVAL;
   const long units = (long)a.B * g.nW * a.heads;
@@ -343,11 +611,7 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     }                                                                                                   \
     hipLaunchKernelGGL(kfn, grid, dim3(256), lds, s, a, g, qsplit);                                     \
   } while (0)
-  if (a.dtype == DFK_BF16) {
-    if (a.hd == 32) LAUNCH_F(bf16raw, 32); else LAUNCH_F(bf16raw, 64);
-  } else {
-    if (a.hd == 32) LAUNCH_F(float, 32); else LAUNCH_F(float, 64);
-  }
+  if (a.hd == 32) LAUNCH_F(float, 32); else LAUNCH_F(float, 64);
 #undef LAUNCH_F
   DFK_CHECK_LAUNCH();
   return 0;
@@ -671,43 +935,6 @@ __global__ __launch_bounds__(256) void wattn_bwd_kernel(const dfk_wattn_bwd_args
 // the dO / Q operands of dV = P^T dO and dK = dS^T Q read with ds_read_tr16
 // from XOR-swizzled tiles, dS crossing the wave's scratch as dS^T (b64 stores,
 // tr16 loads), and a bank-swizzled dQ accumulator.
-
-typedef short short4v __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) short4v lds_short4;
-
-constexpr float kLog2e = 1.4426950408889634f;
-constexpr int kBwdWaves = 8;
-constexpr int kSdStride = 40;  // bf16 row stride of the per-wave dS^T scratch [32 keys][32 queries]
-
-// element offset of (row, col) in a [rows][HD] bf16 tile with 16-B chunks XOR-swizzled by row:
-// conflict-free 16-B row reads (A operands) and 8-B transposed reads (tr16 B operands)
-template <int HD>
-__device__ __forceinline__ int swz(int row, int col) {
-  const int f = HD == 32 ? ((row & 2) | ((row >> 2) & 1)) : (((row & 3) << 1) | ((row >> 2) & 1));
-  return row * HD + (((col >> 3) ^ f) << 3) + (col & 7);
-}
-
-// fp32 [rows][HD] accumulator: the 4 rows a C fragment touches land in two bank halves
-template <int HD>
-__device__ __forceinline__ int dq_off(int row, int col) {
-  return row * HD + (col ^ (((row >> 2) & 1) << 4));
-}
-
-__device__ __forceinline__ bf16x8 tr16x2(const bf16raw* p0, const bf16raw* p1) {
-  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(p0));
-  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(p1));
-  short8 u = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, u);
-}
-
-__device__ __forceinline__ float dot8_bf16(uint4 x, uint4 y) {
-  const bf16raw* a = reinterpret_cast<const bf16raw*>(&x);
-  const bf16raw* b = reinterpret_cast<const bf16raw*>(&y);
-  float d = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) d += bf2f(a[j]) * bf2f(b[j]);
-  return d;
-}
 
 template <int HD, bool RPB, bool MASK>
 __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(const dfk_wattn_bwd_args ba, const Geo g,
