@@ -1,24 +1,35 @@
-// LayerNorm forward/backward over the channel (last) dim — one wave per row.
-// Rows are channels-last token vectors ([B,D,H,W,C] / [B,T,C]), so a row is a
-// contiguous C-vector: 16-byte vector loads, two-pass statistics in registers.
+// LayerNorm forward/backward over the channel (last) dim of channels-last token
+// rows ([B,D,H,W,C] / [B,T,C]): every row is a contiguous C-vector.
+//
+// A row is owned by a group of L lanes (L = 16 / 32 / 64, the smallest power of
+// two covering C/8 16-byte vectors), so a wave handles 64/L rows at once: the
+// Swin stage-1 rows (C = 96 -> 12 vectors) keep 48 of 64 lanes busy instead of
+// 12.  Each lane holds V vectors of 8 channels; row statistics are shuffle
+// reductions inside the group.  Loads are branch-free (out-of-range vectors
+// read the row start and are masked), so every load of a row is in flight at
+// once.  The backward keeps x / dy in registers between its two sweeps when
+// V <= 4, and reduces the dw / db partials group -> wave -> block in LDS with
+// one atomic per channel per block.
 #include "common.h"
 
 namespace {
 
-constexpr int MAXV = 8;  // up to 8 vectors of 8 per lane -> C <= 4096
-
 template <typename T>
-__device__ __forceinline__ void load8(const T* p, float (&v)[8]) {
+__device__ __forceinline__ void load8m(const T* base, long off, bool ok, float (&v)[8]) {
+  const T* p = base + (ok ? off : 0);
   if constexpr (sizeof(T) == 2) {
     uint4 u = *reinterpret_cast<const uint4*>(p);
     const bf16raw* e = reinterpret_cast<const bf16raw*>(&u);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = bf2f(e[i]);
+    for (int i = 0; i < 8; ++i) v[i] = ok ? bf2f(e[i]) : 0.f;
   } else {
-    float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = ok ? v[i] : 0.f;
   }
 }
+
 template <typename T>
 __device__ __forceinline__ void store8(T* p, const float (&v)[8]) {
   if constexpr (sizeof(T) == 2) {
@@ -33,147 +44,221 @@ __device__ __forceinline__ void store8(T* p, const float (&v)[8]) {
   }
 }
 
-template <typename T>
+template <int L>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = L / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, int L, int V>
 __global__ __launch_bounds__(256) void ln_fwd(const T* __restrict__ x, const T* __restrict__ w,
                                               const T* __restrict__ b, T* __restrict__ y, float* mean_out,
                                               float* rstd_out, long rows, int C, float eps) {
-  const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  constexpr int RPW = 64 / L;  // rows per wave
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane % L;
+  const long row = ((long)blockIdx.x * 4 + wave) * RPW + lane / L;
+  const bool rok = row < rows;
   const int nv = C / 8;
-  const T* xr = x + row * C;
-  float v[MAXV][8];
+  const long roff = rok ? row * C : 0;
+  float v[V][8];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int vi = lane + i * 64;
-    if (vi < nv) {
-      load8<T>(xr + vi * 8, v[i]);
+  for (int i = 0; i < V; ++i) {
+    const int vi = li + i * L;
+    load8m<T>(x, roff + vi * 8, rok && vi < nv, v[i]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += v[i][e];
-    }
+    for (int e = 0; e < 8; ++e) s += v[i][e];
   }
-  const float mean = wave_sum(s) / C;
+  const float mean = group_sum<L>(s) / C;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    if (lane + i * 64 < nv) {
+  for (int i = 0; i < V; ++i) {
+    const bool ok = li + i * L < nv;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { const float d = v[i][e] - mean; q += d * d; }
-    }
+    for (int e = 0; e < 8; ++e) { const float d = ok ? v[i][e] - mean : 0.f; q += d * d; }
   }
-  const float rstd = rsqrtf(wave_sum(q) / C + eps);
+  const float rstd = rsqrtf(group_sum<L>(q) / C + eps);
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int vi = lane + i * 64;
-    if (vi < nv) {
-      float wv[8], bv[8], o[8];
-      load8<T>(w + vi * 8, wv);
-      load8<T>(b + vi * 8, bv);
+  for (int i = 0; i < V; ++i) {
+    const int vi = li + i * L;
+    const bool ok = vi < nv;
+    float wv[8], bv[8], o[8];
+    load8m<T>(w, vi * 8, ok, wv);
+    load8m<T>(b, vi * 8, ok, bv);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * wv[e] + bv[e];
-      store8<T>(y + row * C + vi * 8, o);
-    }
+    for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * wv[e] + bv[e];
+    if (rok && ok) store8<T>(y + row * C + vi * 8, o);
   }
-  if (lane == 0) {
+  if (rok && li == 0) {
     if (mean_out) mean_out[row] = mean;
     if (rstd_out) rstd_out[row] = rstd;
   }
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g*xhat)),  g = dy*w ; dw += dy*xhat ; db += dy
-// Two passes over the row (the second re-reads x/dy from L1/L2) keep only the
-// per-lane dw/db partials live across rows.
-constexpr int MAXVB = 6;  // C <= 3072 in the backward
-template <typename T>
+template <typename T, int L, int V>
 __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T* __restrict__ x,
                                               const T* __restrict__ w, const float* __restrict__ mean,
                                               const float* __restrict__ rstd, T* __restrict__ dx, float* dw,
                                               float* db, long rows, int C, int accumulate) {
-  __shared__ float red[2][8 * 64 * MAXVB];
+  constexpr int RPW = 64 / L;
+  constexpr bool KEEP = V <= 4;   // x, dy stay in registers between the two sweeps
+  extern __shared__ float red[];  // [2][C] block partials of dw, db
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane % L;
   const int nv = C / 8;
-  for (int i = threadIdx.x; i < C; i += 256) { red[0][i] = 0.f; red[1][i] = 0.f; }
-  __syncthreads();
-  float pw[MAXVB][8], pb[MAXVB][8];
+  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) red[i] = 0.f;
+  float wv[V][8];
 #pragma unroll
-  for (int i = 0; i < MAXVB; ++i)
+  for (int i = 0; i < V; ++i) load8m<T>(w, (li + i * L) * 8, li + i * L < nv, wv[i]);
+  float pw[V][8], pb[V][8];
+#pragma unroll
+  for (int i = 0; i < V; ++i)
 #pragma unroll
     for (int e = 0; e < 8; ++e) { pw[i][e] = 0.f; pb[i][e] = 0.f; }
-  const long stride = (long)gridDim.x * 4;
-  for (long row = (long)blockIdx.x * 4 + wave; row < rows; row += stride) {
-    const float mu = mean[row], rs = rstd[row];
+  __syncthreads();
+  const long step = (long)gridDim.x * 4 * RPW;
+  for (long r0 = ((long)blockIdx.x * 4 + wave) * RPW; r0 < rows; r0 += step) {
+    const long row = r0 + lane / L;
+    const bool rok = row < rows;
+    const long roff = rok ? row * C : 0;
+    const float mu = mean[rok ? row : 0], rs = rstd[rok ? row : 0];
+    float xs[KEEP ? V : 1][8], ds[KEEP ? V : 1][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXVB; ++i) {
-      const int vi = lane + i * 64;
-      if (vi < nv) {
-        float xv[8], dv[8], wv[8];
-        load8<T>(x + row * C + vi * 8, xv);
-        load8<T>(dy + row * C + vi * 8, dv);
-        load8<T>(w + vi * 8, wv);
+    for (int i = 0; i < V; ++i) {
+      const int vi = li + i * L;
+      const bool ok = rok && vi < nv;
+      float xv[8], dv[8];
+      load8m<T>(x, roff + vi * 8, ok, xv);
+      load8m<T>(dy, roff + vi * 8, ok, dv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xh = (xv[e] - mu) * rs, g = dv[e] * wv[e];
-          s1 += g;
-          s2 += g * xh;
-          pw[i][e] += dv[e] * xh;
-          pb[i][e] += dv[e];
-        }
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (xv[e] - mu) * rs, g = dv[e] * wv[i][e];
+        s1 += g;
+        s2 += g * xh;
+        pw[i][e] += ok ? dv[e] * xh : 0.f;
+        pb[i][e] += dv[e];
+        if constexpr (KEEP) { xs[i][e] = xv[e]; ds[i][e] = dv[e]; }
       }
     }
-    const float m1 = wave_sum(s1) / C, m2 = wave_sum(s2) / C;
+    const float m1 = group_sum<L>(s1) / C, m2 = group_sum<L>(s2) / C;
 #pragma unroll
-    for (int i = 0; i < MAXVB; ++i) {
-      const int vi = lane + i * 64;
-      if (vi < nv) {
-        float xv[8], dv[8], wv[8], o[8];
-        load8<T>(x + row * C + vi * 8, xv);
-        load8<T>(dy + row * C + vi * 8, dv);
-        load8<T>(w + vi * 8, wv);
-        if (accumulate) load8<T>(dx + row * C + vi * 8, o);
+    for (int i = 0; i < V; ++i) {
+      const int vi = li + i * L;
+      const bool ok = rok && vi < nv;
+      float xv[8], dv[8], o[8];
+      if constexpr (KEEP) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xh = (xv[e] - mu) * rs;
-          const float d = rs * (dv[e] * wv[e] - m1 - xh * m2);
-          o[e] = accumulate ? o[e] + d : d;
-        }
-        store8<T>(dx + row * C + vi * 8, o);
+        for (int e = 0; e < 8; ++e) { xv[e] = xs[i][e]; dv[e] = ds[i][e]; }
+      } else {
+        load8m<T>(x, roff + vi * 8, ok, xv);
+        load8m<T>(dy, roff + vi * 8, ok, dv);
       }
+      if (accumulate) load8m<T>(dx, roff + vi * 8, ok, o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (xv[e] - mu) * rs;
+        const float d = rs * (dv[e] * wv[i][e] - m1 - xh * m2);
+        o[e] = accumulate ? o[e] + d : d;
+      }
+      if (ok) store8<T>(dx + row * C + vi * 8, o);
     }
   }
-  for (int wv = 0; wv < 4; ++wv) {
-    if (wave == wv) {
+  // dw / db partials: sum the RPW row groups of the wave, then the waves of the block through LDS
 #pragma unroll
-      for (int i = 0; i < MAXVB; ++i) {
-        const int vi = lane + i * 64;
-        if (vi < nv) {
+  for (int i = 0; i < V; ++i)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) { red[0][vi * 8 + e] += pw[i][e]; red[1][vi * 8 + e] += pb[i][e]; }
-        }
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = L; o < 64; o <<= 1) {
+        pw[i][e] += __shfl_xor(pw[i][e], o, 64);
+        pb[i][e] += __shfl_xor(pb[i][e], o, 64);
+      }
+  for (int wv2 = 0; wv2 < 4; ++wv2) {   // waves in turn: plain read-modify-write, distinct channels per lane
+    if (wave == wv2 && lane < L) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int vi = li + i * L;
+        if (vi < nv)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            red[vi * 8 + e] += pw[i][e];
+            red[C + vi * 8 + e] += pb[i][e];
+          }
       }
     }
     __syncthreads();
   }
-  for (int i = threadIdx.x; i < C; i += 256) {
-    if (dw) atomicAdd(dw + i, red[0][i]);
-    if (db) atomicAdd(db + i, red[1][i]);
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    if (dw) atomicAdd(dw + i, red[i]);
+    if (db) atomicAdd(db + i, red[C + i]);
   }
 }
+
+template <typename T, int L, int V>
+void fwd_launch(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, long rows, int C,
+                float eps, hipStream_t s) {
+  const long per_block = 4L * (64 / L);
+  hipLaunchKernelGGL((ln_fwd<T, L, V>), dim3((unsigned)dfk_cdiv(rows, per_block)), dim3(256), 0, s, (const T*)x,
+                     (const T*)w, (const T*)b, (T*)y, mean, rstd, rows, C, eps);
+}
+
+template <typename T, int L, int V>
+void bwd_launch(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx, float* dw,
+                float* db, long rows, int C, int accumulate, hipStream_t s) {
+  const long per_block = 4L * (64 / L);
+  const int blocks = (int)std::min<long>(2048, dfk_cdiv(rows, per_block));
+  hipLaunchKernelGGL((ln_bwd<T, L, V>), dim3(blocks), dim3(256), 2 * C * sizeof(float), s, (const T*)dy,
+                     (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate);
+}
+
+// (L, V) for C: L = lanes per row, V = 8-channel vectors per lane
+template <typename T, template <typename, int, int> class F, typename... Args>
+bool pick(int C, Args... args) {
+  const int nv = C / 8;
+  if (nv <= 16) { F<T, 16, 1>::run(args...); return true; }
+  if (nv <= 32) { F<T, 32, 1>::run(args...); return true; }
+  switch ((nv + 63) / 64) {
+    case 1: F<T, 64, 1>::run(args...); return true;
+    case 2: F<T, 64, 2>::run(args...); return true;
+    case 3: F<T, 64, 3>::run(args...); return true;
+    case 4: F<T, 64, 4>::run(args...); return true;
+    case 5: F<T, 64, 5>::run(args...); return true;
+    case 6: F<T, 64, 6>::run(args...); return true;
+    case 7: F<T, 64, 7>::run(args...); return true;
+    case 8: F<T, 64, 8>::run(args...); return true;
+    default: return false;
+  }
+}
+
+template <typename T, int L, int V>
+struct Fwd {
+  static void run(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, long rows, int C,
+                  float eps, hipStream_t s) {
+    fwd_launch<T, L, V>(x, w, b, y, mean, rstd, rows, C, eps, s);
+  }
+};
+
+template <typename T, int L, int V>
+struct Bwd {
+  static void run(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
+                  float* dw, float* db, long rows, int C, int accumulate, hipStream_t s) {
+    bwd_launch<T, L, V>(dy, x, w, mean, rstd, dx, dw, db, rows, C, accumulate, s);
+  }
+};
 
 }  // namespace
 
 extern "C" int dfk_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
                                  int64_t rows, int32_t C, float eps, int dtype, hipStream_t s) {
-  if (!x || !w || !b || !y || C % 8 || C > 8 * 64 * MAXV) return DFK_EINVAL;
+  if (!x || !w || !b || !y || C <= 0 || C % 8 || C > 4096) return DFK_EINVAL;
   if (rows <= 0) return 0;
-  dim3 grid(dfk_cdiv(rows, 4));
-  if (dtype == DFK_BF16)
-    hipLaunchKernelGGL(ln_fwd<bf16raw>, grid, dim3(256), 0, s, (const bf16raw*)x, (const bf16raw*)w,
-                       (const bf16raw*)b, (bf16raw*)y, mean, rstd, (long)rows, C, eps);
-  else
-    hipLaunchKernelGGL(ln_fwd<float>, grid, dim3(256), 0, s, (const float*)x, (const float*)w, (const float*)b,
-                       (float*)y, mean, rstd, (long)rows, C, eps);
+  const bool ok = dtype == DFK_BF16 ? pick<bf16raw, Fwd>(C, x, w, b, y, mean, rstd, (long)rows, (int)C, eps, s)
+                                    : pick<float, Fwd>(C, x, w, b, y, mean, rstd, (long)rows, (int)C, eps, s);
+  if (!ok) return DFK_EINVAL;
   DFK_CHECK_LAUNCH();
   return 0;
 }
@@ -181,15 +266,12 @@ extern "C" int dfk_layernorm_fwd(const void* x, const void* w, const void* b, vo
 extern "C" int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                                  void* dx, float* dw, float* db, int64_t rows, int32_t C, int accumulate, int dtype,
                                  hipStream_t s) {
-  if (!dy || !x || !w || !mean || !rstd || !dx || C % 8 || C > 8 * 64 * MAXVB) return DFK_EINVAL;
+  if (!dy || !x || !w || !mean || !rstd || !dx || C <= 0 || C % 8 || C > 4096) return DFK_EINVAL;
   if (rows <= 0) return 0;
-  const int blocks = (int)std::min<int64_t>(1024, (rows + 3) / 4);
-  if (dtype == DFK_BF16)
-    hipLaunchKernelGGL(ln_bwd<bf16raw>, dim3(blocks), dim3(256), 0, s, (const bf16raw*)dy, (const bf16raw*)x,
-                       (const bf16raw*)w, mean, rstd, (bf16raw*)dx, dw, db, (long)rows, C, accumulate);
-  else
-    hipLaunchKernelGGL(ln_bwd<float>, dim3(blocks), dim3(256), 0, s, (const float*)dy, (const float*)x,
-                       (const float*)w, mean, rstd, (float*)dx, dw, db, (long)rows, C, accumulate);
+  const bool ok = dtype == DFK_BF16
+                      ? pick<bf16raw, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, s)
+                      : pick<float, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, s);
+  if (!ok) return DFK_EINVAL;
   DFK_CHECK_LAUNCH();
   return 0;
 }

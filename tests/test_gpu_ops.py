@@ -21,7 +21,8 @@ def tol(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("M,N,Kd", [(1000, 288, 96), (257, 96, 384), (64, 1536, 512), (3, 512, 1024)])
+@pytest.mark.parametrize("M,N,Kd", [(1000, 288, 96), (257, 96, 384), (64, 1536, 512), (3, 512, 1024),
+                                    (1568, 512, 2048), (1592, 768, 3072)])   # last two: automatic split-K slabs
 def test_linear_fwd_bwd(dt, M, N, Kd):
     g = torch.Generator(device=DEV).manual_seed(0)
     x = torch.randn(M, Kd, device=DEV, generator=g).to(dt)
@@ -45,12 +46,17 @@ def test_linear_fwd_bwd(dt, M, N, Kd):
     db = torch.zeros(N, device=DEV)
     K.colsum(dy, db)
     assert rel(db, dy.float().sum(0)) < tol(dt)
-    # gelu' epilogue
-    dh = K.linear_dx(dy, w[:, :Kd], act=2, aux=x) if False else None
+    # bias gradient fused into the dW pass (ones-operand MFMA)
+    dw2 = torch.zeros(N, Kd, device=DEV)
+    db2 = torch.zeros(N, device=DEV)
+    K.linear_dw(dy, x, dw2, db=db2)
+    assert rel(dw2, dy.float().t() @ x.float()) < tol(dt)
+    assert rel(db2, dy.float().sum(0)) < tol(dt)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("rows,C", [(1000, 96), (33, 768), (17, 3072), (5, 512)])
+@pytest.mark.parametrize("rows,C", [(1000, 96), (33, 768), (17, 3072), (5, 512), (1001, 192), (77, 384), (9, 128),
+                                    (13, 1536), (3, 1024), (29, 256)])
 def test_layernorm(dt, rows, C):
     g = torch.Generator(device=DEV).manual_seed(1)
     x = (torch.randn(rows, C, device=DEV, generator=g) * 2 + 0.5).to(dt)
