@@ -71,31 +71,54 @@ def time_kernel(fn, iters):
     return s.elapsed_time(e) / iters * 1e-3   # seconds per launch
 
 
-def roofline(cfg, B, dt, iters):
+ROOFLINE_KERNEL = "wattn_fwd_bf16_kernel<32, true, false>"
+ROOFLINE_PMC = os.path.join(HERE, "profiles", "r1_wattn_fwd_pmc.json")
+
+
+def roofline_case(cfg, B, dt):
     """Dominant MFMA kernel: the stage-1 shifted-window attention core of the Swin-T
-    video backbone at this workload (B clips; window 8x7x7 = 392 tokens, 3 heads x 32).
-    Algorithmic FLOPs per launch = 4 * windows * heads * N^2 * hd (QK^T and PV)."""
+    video backbone at this workload (B clips; window 8x7x7 = 392 tokens, 3 heads x 32,
+    shift (4,3,3), relative-position bias).  Returns (launch fn, algorithmic FLOPs per
+    launch = 4 * windows * heads * N^2 * hd, i.e. QK^T and PV)."""
     from deepfake_amd import kernels as K
     D, H, W = cfg["T"] // 2, cfg["H"] // 4, cfg["W"] // 4
     heads, hd, C = 3, 32, 96
     rows = B * D * H * W
-    qkv = torch.randn(rows, 3 * C, device="cuda").to(dt)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    qkv = torch.randn(rows, 3 * C, device="cuda", generator=g).to(dt)
     win = (8, 7, 7)
     nW = (D // 8) * (H // 7) * (W // 7)
     N = 392
     flops = 4.0 * B * nW * heads * N * N * hd
-    rpb = torch.randn(15 * 13 * 13, heads, device="cuda")
+    rpb = torch.randn(15 * 13 * 13, heads, device="cuda", generator=g) * 0.02
     out = torch.empty(rows, C, device="cuda", dtype=dt)
 
     def run():
         K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, (B, D, H, W), win, win, (4, 3, 3), heads, hd,
                     hd ** -0.5, rpb=rpb, out=out, need_lse=True)
+    return run, flops
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC
+    passes (tools/roofline_pmc.py: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE)."""
+    try:
+        with open(ROOFLINE_PMC) as f:
+            d = json.load(f)
+        return d["bytes_per_launch"], os.path.relpath(ROOFLINE_PMC, HERE)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
+def roofline(cfg, B, dt, iters):
+    run, flops = roofline_case(cfg, B, dt)
     t = time_kernel(run, iters)
     achieved = flops / t / 1e12
-    return {"kernel": "wattn_fwd_kernel<bf16,32> (stage-1 SW-MSA, 392-token windows)", "bound": "mfma",
-            "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-            "flops_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4)}
+    traffic, src = pmc_traffic()
+    return {"kernel": ROOFLINE_KERNEL + " (stage-1 SW-MSA core, 392-token windows, shift 4x3x3, RPB)",
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+            "traffic_source": src, "flops_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4)}
 
 
 def cpu_baseline(cfg_name, steps):
