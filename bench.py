@@ -71,7 +71,7 @@ def time_kernel(fn, iters):
     return s.elapsed_time(e) / iters * 1e-3   # seconds per launch
 
 
-ROOFLINE_KERNEL = "wattn_fwd_bf16_kernel<32, true, false>"
+ROOFLINE_KERNEL = "wattn_fwd_tab_kernel<32>"
 ROOFLINE_PMC = os.path.join(HERE, "profiles", "r1_wattn_fwd_pmc.json")
 
 

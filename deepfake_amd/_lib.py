@@ -41,7 +41,8 @@ class WattnArgs(C.Structure):
                 ("wd", C.c_int32), ("wh", C.c_int32), ("ww", C.c_int32),
                 ("fd", C.c_int32), ("fh", C.c_int32), ("fw", C.c_int32),
                 ("sd", C.c_int32), ("sh", C.c_int32), ("sw", C.c_int32),
-                ("heads", C.c_int32), ("hd", C.c_int32), ("dtype", C.c_int32), ("scale", C.c_float)]
+                ("heads", C.c_int32), ("hd", C.c_int32), ("dtype", C.c_int32), ("scale", C.c_float),
+                ("tab", C.c_void_p)]
 
 
 class WattnBwdArgs(C.Structure):
@@ -68,6 +69,7 @@ SIGNATURES = {
     "dfk_wattn_fwd": [C.POINTER(WattnArgs), _VP],
     "dfk_wattn_bwd": [C.POINTER(WattnBwdArgs), _VP],
     "dfk_wattn_bwd_workspace": [C.POINTER(WattnArgs)],
+    "dfk_wattn_table_workspace": [C.POINTER(WattnArgs)],
     "dfk_patch_im2col": [_VP, C.c_int, _VP, C.c_int, C.POINTER(Im2colArgs), _VP],
     "dfk_patch_merge": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],
     "dfk_rowmean": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],
@@ -81,7 +83,7 @@ SIGNATURES = {
 }
 
 _lib = None
-RESTYPES = {"dfk_wattn_bwd_workspace": _I64, "dfk_gemm_workspace": _I64}
+RESTYPES = {"dfk_wattn_bwd_workspace": _I64, "dfk_wattn_table_workspace": _I64, "dfk_gemm_workspace": _I64}
 
 
 def lib():

@@ -17,6 +17,9 @@ OUT = os.path.join(HERE, "libdfk.so")
 BUILD = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-Wno-unused-result"]
+# attention kernels: MFMA accumulators in VGPRs (no AGPR round trips around the softmax rescale); IEEE
+# mode off with no-NaN semantics so max chains are bare v_max3_f32 (no operand canonicalisation)
+FILE_FLAGS = {"wattn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-honor-nans", "-mno-amdgpu-ieee"]}
 
 
 def _compile(src):
@@ -24,7 +27,7 @@ def _compile(src):
     deps = [src] + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(HERE, "..", "include", "dfk.h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

@@ -521,6 +521,316 @@ __global__ __launch_bounds__(256) void wattn_fwd_bf16_kernel(const dfk_wattn_arg
   }
 }
 
+// ------------------------------------------------------- bias tables (bf16 path)
+// Per (shift class, head): the window's additive score bias in units of the raw product q.k,
+//   (rpb[pos(q) - pos(k) + C0] + (label(q) != label(k) ? -100 : 0)) / scale,   -inf for keys >= N,
+// as fp32, stored in the lane order of the MFMA accumulators it initialises (the C input of S), so
+// the softmax loops read one 16-B vector per lane per tile and never gather, decode or compare:
+//   fwd (key on the accumulator row, query on the lane): [c][h][Np/16][Np/32][64 lanes][8]
+//       slot j = 4*h2 + r  <->  q = 16*qt + (lane&15),  k = 32*kb + 16*h2 + 4*(lane>>4) + r
+//   bwd (query on the row, key on the lane):             [c][h][Np/32][Np/32][64 lanes][16]
+//       slot j = 8*qh + 4*h2 + r  <->  q = 32*qb + 16*qh + 4*(lane>>4) + r,  k = 32*kb + 16*h2 + (lane&15)
+// Shift class: one bit per shifted dim, set for the last window along it — the only window whose
+// tokens straddle two regions of compute_mask (video_swin_transformer.py:319-333); interior windows
+// are class 0 (no mask).  Labels and RPB positions are arithmetic (Q3: positions decode with the full
+// window geometry; Q4: -100, not -inf).
+struct TabGeo {
+  int ncls;      // 8 when any shift > 0, else 1
+  long per_ch;   // fwd (= bwd) entries per (class, head) = Np * Np
+};
+
+// table-kernel token record: RPB position << 3 | straddle bits (d, h, w: the token lies past the region
+// split of the last window along that dim)
+__device__ __forceinline__ int tab_token(const dfk_wattn_args& a, int i) {
+  const int fd = i / (a.fh * a.fw), fh = (i / a.fw) % a.fh, fw = i % a.fw;
+  const int pos = (fd * (2 * a.fh - 1) + fh) * (2 * a.fw - 1) + fw;
+  const int td = i / (a.wh * a.ww), th = (i / a.ww) % a.wh, tw = i % a.ww;
+  const int bits = (a.sd > 0 && td >= a.wd - a.sd ? 4 : 0) | (a.sh > 0 && th >= a.wh - a.sh ? 2 : 0) |
+                   (a.sw > 0 && tw >= a.ww - a.sw ? 1 : 0);
+  return pos << 3 | bits;
+}
+
+// Block (chunk, class*heads + head): token records and the head's RPB column (/ scale) in LDS, then
+// one thread per 16-B lane slot of the fwd layout (8 values) or 32-B slot of the bwd layout (16).
+__global__ __launch_bounds__(256) void wattn_tab_kernel(const dfk_wattn_args a, const Geo g, long nf, long nb,
+                                                        float* __restrict__ tf, float* __restrict__ tb) {
+  extern __shared__ int tsm[];
+  int* tok = tsm;                                          // [Np]
+  float* rp = reinterpret_cast<float*>(tsm + g.Np);        // [L]
+  const int ch = blockIdx.y, h = ch % a.heads, cls = ch / a.heads;
+  const float inv_scale = 1.f / a.scale, pen = -100.f * inv_scale;
+  for (int i = threadIdx.x; i < g.Np; i += blockDim.x) tok[i] = i < g.N ? tab_token(a, i) : 0;
+  for (int l = threadIdx.x; l < g.L; l += blockDim.x) rp[l] = a.rpb ? a.rpb[(long)l * a.heads + h] * inv_scale : 0.f;
+  __syncthreads();
+  auto val = [&](int q, int k) -> float {
+    if (k >= g.N) return -INFINITY;
+    if (q >= g.N) return 0.f;
+    const int tq = tok[q], tk = tok[k];
+    float v = rp[(tq >> 3) - (tk >> 3) + g.C0];
+    if ((tq ^ tk) & cls & 7) v += pen;
+    return v;
+  };
+  const int nq16 = g.Np / 16, nk32 = g.Np / 32;
+  const long per_f = (long)nq16 * nk32 * 64, per_b = (long)nk32 * nk32 * 64;   // slots per (class, head)
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < per_f + (nb ? per_b : 0);
+       t += (long)gridDim.x * blockDim.x) {
+    const int lane = (int)(t & 63), grp = lane >> 4, ql = lane & 15;
+    if (t < per_f) {
+      const long u = t >> 6;
+      const int kb = (int)(u % nk32), qt = (int)(u / nk32);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = val(qt * 16 + ql, kb * 32 + (j >> 2) * 16 + grp * 4 + (j & 3));
+      float* dst = tf + (ch * per_f + t) * 8;
+      *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      const long tt = t - per_f, u = tt >> 6;
+      const int kb = (int)(u % nk32), qb = (int)(u / nk32);
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = val(qb * 32 + (j >> 3) * 16 + grp * 4 + (j & 3), kb * 32 + ((j >> 2) & 1) * 16 + ql);
+      float* dst = tb + (ch * per_b + tt) * 16;
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) *reinterpret_cast<float4*>(dst + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+    }
+  }
+}
+
+TabGeo tab_geo(const dfk_wattn_args& a, const Geo& g) {
+  TabGeo t;
+  t.ncls = g.use_mask ? 8 : 1;
+  t.per_ch = (long)g.Np * g.Np;
+  return t;
+}
+
+// table elements (fp32) of one layout
+long tab_elems(const dfk_wattn_args& a, const Geo& g) {
+  const TabGeo t = tab_geo(a, g);
+  return (long)t.ncls * a.heads * t.per_ch;
+}
+
+// Work order of the table kernels: units sorted by (shift class, head, clip, window) and dealt to the
+// XCDs in contiguous chunks (blocks b and b+8 share an XCD), so the workgroups that read one (class,
+// head) table run together on one XCD and the table is read from that XCD's L2.
+struct WUnit {
+  int b, win, head, cls, qpart;
+  long lse_unit;   // (b*nW + win)*heads + head: the lse row, as the table-free kernels index it
+};
+
+__device__ __forceinline__ WUnit decode_unit(const dfk_wattn_args& a, const Geo& g, int qsplit) {
+  const int total = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, per = total >> 3, rr = total & 7;
+  int u = (xcd < rr ? xcd * (per + 1) : rr * (per + 1) + (xcd - rr) * per) + (bid >> 3);
+  WUnit w;
+  w.qpart = u % qsplit;
+  u /= qsplit;
+  const int ncls = g.use_mask ? 8 : 1;
+  int c = 0, nd = g.nwd, nh = g.nwh, nw = g.nww;
+  for (; c < ncls; ++c) {
+    nd = g.use_mask ? ((c & 4) ? (a.sd > 0) : g.nwd - (a.sd > 0)) : g.nwd;
+    nh = g.use_mask ? ((c & 2) ? (a.sh > 0) : g.nwh - (a.sh > 0)) : g.nwh;
+    nw = g.use_mask ? ((c & 1) ? (a.sw > 0) : g.nww - (a.sw > 0)) : g.nww;
+    const int cnt = nd * nh * nw * a.B * a.heads;
+    if (u < cnt) break;
+    u -= cnt;
+  }
+  const int perw = nd * nh * nw;
+  w.head = u / (perw * a.B);
+  u %= perw * a.B;
+  w.b = u / perw;
+  u %= perw;
+  const int id = u / (nh * nw), ih = (u / nw) % nh, iw = u % nw;
+  const int wdi = (c & 4) ? g.nwd - 1 : id, whi = (c & 2) ? g.nwh - 1 : ih, wwi = (c & 1) ? g.nww - 1 : iw;
+  w.win = (wdi * g.nwh + whi) * g.nww + wwi;
+  w.cls = c;
+  w.lse_unit = ((long)w.b * g.nW + w.win) * a.heads + w.head;
+  return w;
+}
+
+// wattn.hip is compiled with IEEE mode off and no-NaN semantics (build.py FILE_FLAGS), so fmaxf chains
+// become v_max3_f32 without operand canonicalisation.
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+
+// max over the 4 lane groups (lanes l, l^16, l^32, l^48) by the gfx950 row / half swaps
+__device__ __forceinline__ float grp_max4(float v) {
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float m = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  return fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+}
+
+// Forward with the bias table.  Work order: decode_unit (class/head-sorted, XCD-chunked).  One
+// workgroup = one (clip, window, head): K/V staged once into swizzled LDS tiles (the only LDS: three
+// workgroups fit a CU at 392-token windows); per wave 32 queries against 32-key blocks: S^T = K Q^T +
+// table (the fp32 table tile is loaded straight into the accumulators, two key blocks ahead), running
+// max in raw units, P = 2^(S*scale*log2e - m) by one fma + exp per score, lazy rescale,
+// O^T += V^T P^T, l = ones^T P^T (the denominator on the MFMA too).
+template <int HD>
+__global__ __launch_bounds__(256) void wattn_fwd_tab_kernel(const dfk_wattn_args a, const Geo g, int qsplit,
+                                                            const float* __restrict__ tab) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16raw* Ks = reinterpret_cast<bf16raw*>(smem);
+  bf16raw* Vs = Ks + (size_t)g.Np * HD;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = lane >> 4, ql = lane & 15, tq = ql >> 2, tp = ql & 3;
+  const WUnit wu = decode_unit(a, g, qsplit);
+  const int head = wu.head, win = wu.win, b = wu.b;
+  const long unit = wu.lse_unit;
+  const int hoff = head * HD;
+  constexpr int CH = HD / 8;
+  for (int idx = tid; idx < g.Np * CH; idx += blockDim.x) {
+    const int i = idx / CH, c = (idx % CH) * 8;
+    const int row = token_info_row(a, g, b, win, i);
+    *reinterpret_cast<uint4*>(Ks + swz<HD>(i, c)) = tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + c);
+    *reinterpret_cast<uint4*>(Vs + swz<HD>(i, c)) = tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + c);
+  }
+  const int nkb = g.Np / 32, nqb = g.Np / 32;
+  const float* tch = tab + ((long)wu.cls * a.heads + head) * (long)g.Np * g.Np;
+  __syncthreads();
+
+  const float scale2 = a.scale * kLog2e;
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+  const int nw = blockDim.x >> 6;
+  // Q fragments of the wave's next query block are loaded one block ahead (their latency hides under
+  // the current block's key sweep)
+  int qrown[2];
+  bf16x8 qfn[2][HD / 32];
+  auto load_q = [&](int qb) {
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const int q = qb * 32 + qh * 16 + ql;
+      qrown[qh] = q < g.N ? token_info_row(a, g, b, win, q) : -2;
+#pragma unroll
+      for (int es = 0; es < HD / 32; ++es)
+        qfn[qh][es] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.q, a.pad_q, qrown[qh], a.ld_qkv, hoff + es * 32 + grp * 8));
+    }
+  };
+  const int qstep = nw * qsplit;
+  load_q(min(wu.qpart * nw + wave, nqb - 1));
+  for (int qb = wu.qpart * nw + wave; qb < nqb; qb += qstep) {
+    int qrow[2];
+    bf16x8 qf[2][HD / 32];
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      qrow[qh] = qrown[qh];
+#pragma unroll
+      for (int es = 0; es < HD / 32; ++es) qf[qh][es] = qfn[qh][es];
+    }
+    load_q(min(qb + qstep, nqb - 1));
+    // the lane's table slots: [qt][kb][lane][8 floats], qt = 2 qb + qh
+    const f32x4* tq0 = reinterpret_cast<const f32x4*>(tch) + ((long)(qb * 2) * nkb * 64 + lane) * 2;
+    const long tqh = (long)nkb * 64 * 2;   // f32x4 stride between the two query halves
+    auto load_tab = [&](f32x4 (&s)[2][2], int kb) {
+      const f32x4* p = tq0 + (long)kb * 128;
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        s[qh][0] = p[qh * tqh];
+        s[qh][1] = p[qh * tqh + 1];
+      }
+    };
+    float m2[2] = {-INFINITY, -INFINITY};   // running max of S * scale * log2e
+    f32x4 o[2][HD / 16], lsum[2];
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      lsum[qh] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et) o[qh][et] = f32x4{0, 0, 0, 0};
+    }
+    // per key block: S = K Q^T onto the table tile (qk), softmax + O/l update (soft); the table tile of
+    // block kb+2 streams into the freed accumulators right after the exponentials
+    auto qk = [&](f32x4 (&s)[2][2], int kb) {
+      bf16x8 ka[2][HD / 32];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int es = 0; es < HD / 32; ++es)
+          ka[h2][es] = *reinterpret_cast<const bf16x8*>(Ks + swz<HD>(kb * 32 + h2 * 16 + ql, es * 32 + grp * 8));
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+          for (int es = 0; es < HD / 32; ++es)
+            s[qh][h2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[h2][es], qf[qh][es], s[qh][h2], 0, 0, 0);
+    };
+    auto soft = [&](f32x4 (&s)[2][2], int kb) {
+      bool grow = false;
+      float mnew[2];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        const float x0 = max3f(s[qh][0][0], s[qh][0][1], s[qh][0][2]);
+        const float x1 = max3f(s[qh][0][3], s[qh][1][0], s[qh][1][1]);
+        const float x2 = max3f(s[qh][1][2], s[qh][1][3], x0);
+        const float mx = grp_max4(fmaxf(x1, x2)) * scale2;
+        mnew[qh] = mx > m2[qh] + kRescale ? mx : m2[qh];
+        grow |= mnew[qh] != m2[qh];
+      }
+      if (__builtin_amdgcn_ballot_w64(grow) != 0) {
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const float alpha = m2[qh] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m2[qh] - mnew[qh]);
+          m2[qh] = mnew[qh];
+          lsum[qh] *= alpha;
+#pragma unroll
+          for (int et = 0; et < HD / 16; ++et) o[qh][et] *= alpha;
+        }
+      }
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            pf[qh][h2 * 4 + r] = (__bf16)__builtin_amdgcn_exp2f(__builtin_fmaf(s[qh][h2][r], scale2, -m2[qh]));
+      load_tab(s, min(kb + 2, nkb - 1));   // unconditional (clamped): static vmcnt counts, no phi copies
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et) {
+        const int c = et * 16 + tp * 4;
+        const bf16x8 va = tr16x2(Vs + swz<HD>(kb * 32 + grp * 4 + tq, c), Vs + swz<HD>(kb * 32 + 16 + grp * 4 + tq, c));
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) o[qh][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pf[qh], o[qh][et], 0, 0, 0);
+      }
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qh], lsum[qh], 0, 0, 0);
+    };
+    f32x4 sA[2][2], sB[2][2];
+    load_tab(sA, 0);
+    load_tab(sB, min(1, nkb - 1));
+    int kb = 0;
+    for (; kb + 1 < nkb; kb += 2) {
+      qk(sA, kb);
+      soft(sA, kb);
+      qk(sB, kb + 1);
+      soft(sB, kb + 1);
+    }
+    if (kb < nkb) {
+      qk(sA, kb);
+      soft(sA, kb);
+    }
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const int q = qb * 32 + qh * 16 + ql;
+      const float l = lsum[qh][0];
+      const float inv = 1.f / l;
+      if (qrow[qh] >= 0) {
+        bf16raw* op = reinterpret_cast<bf16raw*>(a.out) + (long)qrow[qh] * a.ld_out + hoff;
+#pragma unroll
+        for (int et = 0; et < HD / 16; ++et) {
+          uint2 u;
+          u.x = (uint32_t)f2bf(o[qh][et][0] * inv) | ((uint32_t)f2bf(o[qh][et][1] * inv) << 16);
+          u.y = (uint32_t)f2bf(o[qh][et][2] * inv) | ((uint32_t)f2bf(o[qh][et][3] * inv) << 16);
+          *reinterpret_cast<uint2*>(op + et * 16 + grp * 4) = u;
+        }
+      }
+      if (a.lse && grp == 0 && q < g.N) a.lse[unit * g.Np + q] = (m2[qh] + __log2f(l)) * 0.6931471805599453f;
+    }
+  }
+}
+
 size_t fwd_lds_bf16(const dfk_wattn_args& a, const Geo& g) {
   return 16 + 4 * (size_t)g.Np + 4 * (size_t)((g.L + 3) & ~3) + 4 * (size_t)g.Np * a.hd;
 }
@@ -564,6 +874,35 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
   if (!ap || !args_ok(*ap)) return DFK_EINVAL;
   const dfk_wattn_args& a = *ap;
   const Geo g = make_geo(a);
+  if (a.dtype == DFK_BF16 && a.tab && !a.mask && a.scale > 0.f) {
+    const long units = (long)a.B * g.nW * a.heads;
+    if (units <= 0) return 0;
+    const TabGeo tg = tab_geo(a, g);
+    const long nb = 0;   // the backward does not read the bwd layout yet
+    float* tf = reinterpret_cast<float*>(a.tab);
+    const long slots = tg.per_ch / 8 + (nb ? tg.per_ch / 16 : 0);
+    hipLaunchKernelGGL(wattn_tab_kernel, dim3((unsigned)std::min<long>(dfk_cdiv(slots, 256), 64), tg.ncls * a.heads),
+                       dim3(256), 4 * (size_t)(g.Np + g.L), s, a, g, tg.per_ch / 8, nb, tf, tf + tab_elems(a, g));
+    const size_t lds = 4 * (size_t)g.Np * a.hd;
+    const int nqb = g.Np / 32;
+    const int nw = std::min(4, nqb);
+    const int qsplit = (int)std::max<long>(1, std::min<long>(dfk_cdiv(nqb, nw), dfk_cdiv(1024, units)));
+    dim3 grid((unsigned)(units * qsplit));
+#define LAUNCH_T(HD)                                                                                         \
+  do {                                                                                                       \
+    auto kfn = wattn_fwd_tab_kernel<HD>;                                                                     \
+    static bool attr_set = false;                                                                            \
+    if (!attr_set) {                                                                                         \
+      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);   \
+      attr_set = true;                                                                                       \
+    }                                                                                                        \
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), lds, s, a, g, qsplit, (const float*)tf);                 \
+  } while (0)
+    if (a.hd == 32) LAUNCH_T(32); else LAUNCH_T(64);
+#undef LAUNCH_T
+    DFK_CHECK_LAUNCH();
+    return 0;
+  }
   if (a.dtype == DFK_BF16) {
     const size_t lds = fwd_lds_bf16(a, g);
     if (lds > 160 * 1024) return DFK_EINVAL;
@@ -1362,6 +1701,13 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
   reduce_drpb(*bp, g, units, s);
   DFK_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int64_t dfk_wattn_table_workspace(const dfk_wattn_args* f) {
+  if (!f || !args_ok(*f)) return -1;
+  if (f->dtype != DFK_BF16 || f->mask) return 0;
+  const Geo g = make_geo(*f);
+  return 4 * 2 * tab_elems(*f, g);   // fwd + bwd layouts, fp32
 }
 
 extern "C" int64_t dfk_wattn_bwd_workspace(const dfk_wattn_args* f) {

@@ -185,8 +185,9 @@ class WindowAttnFn(torch.autograd.Function):
             bc = compute_weight(qkv_bias, qkv.dtype)
             pads = (bc[:C], bc[C:2 * C], bc[2 * C:])
         rpb_f = rpb.detach().float().contiguous() if rpb is not None else None
-        out, lse = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], qkv.stride(0), dims, window, full_window, shift, heads,
-                               hd, scale, rpb=rpb_f, pads=pads, mask=mask)
+        out, lse, tab = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], qkv.stride(0), dims, window, full_window, shift,
+                                    heads, hd, scale, rpb=rpb_f, pads=pads, mask=mask, return_table=True)
+        ctx.tab = tab
         grad_use(ctx, 1, rpb)
         grad_use(ctx, 2, qkv_bias)
         ctx.save_for_backward(qkv, out, lse, rpb_f, mask, rpb, qkv_bias)
@@ -207,7 +208,8 @@ class WindowAttnFn(torch.autograd.Function):
         dpads = [dbias[i * C:(i + 1) * C] for i in range(3)] if ctx.has_bias else None
         K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, qkv.stride(0), dims, window, full_window, shift, heads,
                      hd, scale, rpb_f, ctx.pads), dout.contiguous(), dqkv, dqkv[:, C:], dqkv[:, 2 * C:], qkv.stride(0),
-                    drpb=drpb, dpads=dpads, mask=mask)
+                    drpb=drpb, dpads=dpads, mask=mask, tab=ctx.tab)
+        ctx.tab = None
         if ctx.has_rpb:
             drpb = grad_done(rpb, drpb)
         if ctx.has_bias:

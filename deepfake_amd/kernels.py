@@ -5,6 +5,7 @@ the torch caching allocator (graph-capture safe) and raises on any error.
 Activations are 2-D token-major views ([rows, C], contiguous rows).
 """
 import math
+import os
 
 import torch
 
@@ -156,24 +157,38 @@ def window_geometry(dims, window):
 
 
 def wattn_fwd(q, k, v, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb=None, pads=None,
-              out=None, need_lse=True, mask=None):
-    """Token-major window attention core; returns (out [rows, heads*hd], lse)."""
+              out=None, need_lse=True, mask=None, use_table=True, return_table=False):
+    """Token-major window attention core; returns (out [rows, heads*hd], lse[, tab]).
+    use_table: bf16 score-bias tables (RPB + shift mask per shift class, dfk_wattn_table_workspace);
+    the backward must be handed the same `tab`."""
     rows = dims[0] * dims[1] * dims[2] * dims[3]
     if out is None:
         out = torch.empty(rows, heads * hd, device=q.device, dtype=q.dtype)
     nW, N, Np = window_geometry(dims, window)
     lse = torch.empty(dims[0] * nW * heads, Np, device=q.device, dtype=torch.float32) if need_lse else None
     a = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse, mask)
+    tab = None
+    if use_table and os.environ.get("DFK_WATTN_TABLE", "1") != "0":
+        nbytes = L.lib().dfk_wattn_table_workspace(a)
+        if nbytes < 0:
+            raise RuntimeError("dfk_wattn_table_workspace: invalid arguments")
+        if nbytes > 0:
+            tab = torch.empty(nbytes // 4, device=q.device, dtype=torch.float32)
+            a.tab = tab.data_ptr()
     L.check(L.lib().dfk_wattn_fwd(a, L.stream()), "wattn_fwd")
+    if return_table:
+        return out, lse, tab
     return out, lse
 
 
-def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None, mask=None):
+def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None, mask=None, tab=None):
     """Backward of wattn_fwd.  fwd_args_tensors = (q, k, v, out, lse, ld_qkv, dims, window, full_window,
     shift, heads, hd, scale, rpb, pads).  dq/dk/dv may alias column slices of one [rows, 3C] buffer."""
     (q, k, v, out, lse, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads) = fwd_args_tensors
     ba = L.WattnBwdArgs()
     ba.f = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse, mask)
+    if tab is not None:
+        ba.f.tab = tab.data_ptr()
     ba.dout = dout.data_ptr()
     ba.dq, ba.dk, ba.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
     ba.drpb = drpb.data_ptr() if drpb is not None else None

@@ -111,7 +111,12 @@ int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float*
  *   explicit additive mask [mask_nw, N, N] fp32 (WindowAttention3D.forward's
  *   `mask` argument, :160-163) indexed by (clip-window index) % mask_nw.
  *   scale multiplies q before q k^T (Q5).
- *   lse (fp32 [B*nW, nH, Np]) saved for the backward. */
+ *   lse (fp32 [B*nW, nH, Np]) saved for the backward.
+ *   tab: bf16 path only (NULL = table-free kernels): device scratch of
+ *   dfk_wattn_table_workspace() bytes.  dfk_wattn_fwd writes the per-(shift
+ *   class, head) score-bias tables there (RPB + shift mask, fp16, in MFMA
+ *   accumulator order); dfk_wattn_bwd reads them, so the backward must get the
+ *   same buffer, untouched, with the same rpb. */
 typedef struct {
   const void* q; const void* k; const void* v;
   void* out;
@@ -128,8 +133,10 @@ typedef struct {
   int32_t heads, hd;
   int32_t dtype;
   float scale;
+  void* tab;
 } dfk_wattn_args;
 int dfk_wattn_fwd(const dfk_wattn_args* a, hipStream_t stream);
+int64_t dfk_wattn_table_workspace(const dfk_wattn_args* a);
 /* backward: f is the forward's argument block (f.out = the forward output O,
  * f.lse its log-sum-exp).  dq/dk/dv are written (=) at the q/k/v layout with
  * row stride ld_dqkv; drpb [L,nH] fp32 (+=); gradients of padded positions
