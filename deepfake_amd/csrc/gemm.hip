@@ -1,7 +1,7 @@
 // Generic MFMA GEMM for gfx950 with operand views (plain / k-major / implicit
 // conv), batching, split-K and fused epilogues.  See include/dfk.h.
 //
-// Tile 128x128 per 256-thread workgroup (4 waves, 2x2, 64x64 each).
+// Tile 128x128 (or 64x64 for grids too small to fill the chip) per 256-thread workgroup (4 waves, 2x2).
 //   bf16: v_mfma_f32_16x16x32_bf16, BK = 64 (2 MFMA k-steps per staged tile)
 //   f32 : v_mfma_f32_16x16x4_f32   (exact fp32, parity mode), BK = 32
 // Staging: global -> registers (16-B vectors along each view's contiguous dim)
@@ -16,7 +16,7 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 128, NT = 256;
+constexpr int NT = 256;   // 4 waves (2 x 2), wave tile WT x WT, workgroup tile 2WT x 2WT
 
 template <typename T> struct GT;
 template <> struct GT<bf16raw> { static constexpr int BK = 64, VEC = 8, PADR = 8, PADK = 16; };
@@ -81,12 +81,14 @@ __device__ __forceinline__ uint4 view_load(const T* base, const dfk_view& v, lon
 }
 
 // stage one ROWS x BK operand tile: global -> 4 x 16-B registers per thread
+template <typename T, int ROWS> constexpr int tile_vecs() { return ROWS * GT<T>::BK / (NT * GT<T>::VEC); }
+
 template <typename T, bool KMAJ, int ROWS, bool VECOK, bool CONV>
 __device__ __forceinline__ void load_tile(const T* base, const dfk_view& v, int row0, int rowlim, int k0, int klim,
-                                          int tid, uint4 (&r)[4]) {
+                                          int tid, uint4 (&r)[tile_vecs<T, ROWS>()]) {
   constexpr int TBK = GT<T>::BK, VEC = GT<T>::VEC;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < tile_vecs<T, ROWS>(); ++s) {
     const int idx = tid + s * NT;
     if constexpr (!KMAJ) {   // view rows = tile rows, contiguous along k
       const int i = idx / (TBK / VEC), kc = idx % (TBK / VEC);
@@ -101,11 +103,11 @@ __device__ __forceinline__ void load_tile(const T* base, const dfk_view& v, int 
 }
 
 template <typename T, bool KMAJ, int ROWS>
-__device__ __forceinline__ void store_tile(T* lds, int tid, const uint4 (&r)[4]) {
+__device__ __forceinline__ void store_tile(T* lds, int tid, const uint4 (&r)[tile_vecs<T, ROWS>()]) {
   using TL = Tile<T, KMAJ, ROWS>;
   constexpr int TBK = GT<T>::BK, VEC = GT<T>::VEC;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < tile_vecs<T, ROWS>(); ++s) {
     const int idx = tid + s * NT;
     if constexpr (!KMAJ) {
       const int i = idx / (TBK / VEC), kc = idx % (TBK / VEC);
@@ -196,14 +198,16 @@ __device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1
   }
 }
 
-template <typename T, bool AK, bool BKM, bool VECOK, bool CONV, bool RS = false>
+template <typename T, int WT, bool AK, bool BKM, bool VECOK, bool CONV, bool RS = false>
 __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int evec, float* slab) {
+  constexpr int BM = 2 * WT, BN = 2 * WT, MI = WT / 16;
+  constexpr int VA = tile_vecs<T, BM>(), VB = tile_vecs<T, BN>();
   using TA = Tile<T, AK, BM>;
   using TB = Tile<T, BKM, BN>;
   constexpr int TBK = GT<T>::BK;
   constexpr int BUF = TA::ELEMS + TB::ELEMS;
-  constexpr int ES = 64 + 4;                      // epilogue staging row stride (fp32)
-  constexpr int SMEM_T = 2 * BUF > (4 * 64 * ES * 4) / (int)sizeof(T) ? 2 * BUF : (4 * 64 * ES * 4) / (int)sizeof(T);
+  constexpr int ES = WT + 4;                      // epilogue staging row stride (fp32)
+  constexpr int SMEM_T = 2 * BUF > (4 * WT * ES * 4) / (int)sizeof(T) ? 2 * BUF : (4 * WT * ES * 4) / (int)sizeof(T);
   __shared__ __attribute__((aligned(16))) T smem[SMEM_T];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -227,98 +231,112 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
   const int kbeg = split * kchunk;
   const int kend = min(g.K, kbeg + kchunk);
 
-  f32x4 acc[4][4];
+  f32x4 acc[MI][MI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // fused row sums of A (bias gradients): one wave column of the first N-tile multiplies A by ones
   const bool do_rs = RS && tn == 0 && wn == 0;   // RS: instantiated only for the dW (k-major x k-major) GEMM
-  f32x4 accr[4];
+  f32x4 accr[MI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) accr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MI; ++i) accr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[4], rb[4];
-  if (kbeg < kend) {
-    load_tile<T, AK, BM, VECOK, CONV>(A, g.a, bm, g.M, kbeg, kend, tid, ra);
-    load_tile<T, BKM, BN, VECOK, CONV>(B, g.b, bn, g.N, kbeg, kend, tid, rb);
-    store_tile<T, AK, BM>(smem, tid, ra);
-    store_tile<T, BKM, BN>(smem + TA::ELEMS, tid, rb);
+  // register ring of PF staged k-tiles in flight (loads are unconditional: past kend they are masked
+  // to zero by the view bounds), LDS double buffer: tile t is computed from LDS[t&1] while tile t+1
+  // moves from its registers into LDS[(t+1)&1] and tile t+1+PF is requested into the freed registers.
+  constexpr int PF = WT == 32 ? 4 : 1;
+  uint4 ra[PF][VA], rb[PF][VB];
+  const int ntile = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
+#pragma unroll
+  for (int d = 0; d < PF; ++d) {
+    const int kd = kbeg + max(0, min(d, ntile - 1)) * TBK;
+    load_tile<T, AK, BM, VECOK, CONV>(A, g.a, bm, g.M, kd, kend, tid, ra[d]);
+    load_tile<T, BKM, BN, VECOK, CONV>(B, g.b, bn, g.N, kd, kend, tid, rb[d]);
+  }
+  store_tile<T, AK, BM>(smem, tid, ra[0]);
+  store_tile<T, BKM, BN>(smem + TA::ELEMS, tid, rb[0]);
+  {
+    const int kd = kbeg + max(0, min(PF, ntile - 1)) * TBK;
+    load_tile<T, AK, BM, VECOK, CONV>(A, g.a, bm, g.M, kd, kend, tid, ra[0]);
+    load_tile<T, BKM, BN, VECOK, CONV>(B, g.b, bn, g.N, kd, kend, tid, rb[0]);
   }
   __syncthreads();
-  int cur = 0;
-  for (int k0 = kbeg; k0 < kend; k0 += TBK) {
-    const bool more = k0 + TBK < kend;
-    if (more) {
-      load_tile<T, AK, BM, VECOK, CONV>(A, g.a, bm, g.M, k0 + TBK, kend, tid, ra);
-      load_tile<T, BKM, BN, VECOK, CONV>(B, g.b, bn, g.N, k0 + TBK, kend, tid, rb);
-    }
-    const T* As = smem + cur * BUF;
-    const T* Bs = As + TA::ELEMS;
-    if constexpr (sizeof(T) == 2) {
+  for (int t0 = 0; t0 < ntile; t0 += PF) {
 #pragma unroll
-      for (int ks = 0; ks < TBK / 32; ++ks) {
-        bf16x8 af[4], bfr[4];
+    for (int d = 0; d < PF; ++d) {
+      const int t = t0 + d;
+      if (t >= ntile) break;
+      const T* As = smem + (t & 1) * BUF;
+      const T* Bs = As + TA::ELEMS;
+      if constexpr (sizeof(T) == 2) {
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) af[mi] = frag_bf16<AK, BM>(As, wm * 64 + mi * 16, ks * 32, lane);
+        for (int ks = 0; ks < TBK / 32; ++ks) {
+          bf16x8 af[MI], bfr[MI];
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) bfr[ni] = frag_bf16<BKM, BN>(Bs, wn * 64 + ni * 16, ks * 32, lane);
+          for (int mi = 0; mi < MI; ++mi) af[mi] = frag_bf16<AK, BM>(As, wm * WT + mi * 16, ks * 32, lane);
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+          for (int ni = 0; ni < MI; ++ni) bfr[ni] = frag_bf16<BKM, BN>(Bs, wn * WT + ni * 16, ks * 32, lane);
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
-        if (RS && do_rs) {
-          bf16x8 ones;
+          for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+            for (int ni = 0; ni < MI; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+          if (RS && do_rs) {
+            bf16x8 ones;
 #pragma unroll
-          for (int mi = 0; mi < 4; ++mi) accr[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], ones, accr[mi], 0, 0, 0);
+            for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+#pragma unroll
+            for (int mi = 0; mi < MI; ++mi) accr[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], ones, accr[mi], 0, 0, 0);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < TBK / 4; ++ks) {
+          float af[MI], bfr[MI];
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi) af[mi] = frag_f32<AK, BM>(As, wm * WT + mi * 16, ks * 4, lane);
+#pragma unroll
+          for (int ni = 0; ni < MI; ++ni) bfr[ni] = frag_f32<BKM, BN>(Bs, wn * WT + ni * 16, ks * 4, lane);
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < MI; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+          if (RS && do_rs)
+#pragma unroll
+            for (int mi = 0; mi < MI; ++mi) accr[mi] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi], 1.0f, accr[mi], 0, 0, 0);
         }
       }
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < TBK / 4; ++ks) {
-        float af[4], bfr[4];
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) af[mi] = frag_f32<AK, BM>(As, wm * 64 + mi * 16, ks * 4, lane);
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) bfr[ni] = frag_f32<BKM, BN>(Bs, wn * 64 + ni * 16, ks * 4, lane);
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
-        if (RS && do_rs)
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) accr[mi] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi], 1.0f, accr[mi], 0, 0, 0);
-      }
+      const int nx = (d + 1) % PF;   // static after the full unroll
+      if (PF == 1 && t + 1 >= ntile) break;   // single stage: no trailing re-request (uniform)
+      store_tile<T, AK, BM>(smem + ((t + 1) & 1) * BUF, tid, ra[nx]);
+      store_tile<T, BKM, BN>(smem + ((t + 1) & 1) * BUF + TA::ELEMS, tid, rb[nx]);
+      __syncthreads();
+      const int kn = kbeg + min(t + 1 + PF, ntile - 1) * TBK;   // past the end: re-request the last tile (L2 hit)
+      load_tile<T, AK, BM, VECOK, CONV>(A, g.a, bm, g.M, kn, kend, tid, ra[nx]);
+      load_tile<T, BKM, BN, VECOK, CONV>(B, g.b, bn, g.N, kn, kend, tid, rb[nx]);
     }
-    if (more) {
-      store_tile<T, AK, BM>(smem + (cur ^ 1) * BUF, tid, ra);
-      store_tile<T, BKM, BN>(smem + (cur ^ 1) * BUF + TA::ELEMS, tid, rb);
-    }
-    __syncthreads();
-    cur ^= 1;
   }
 
   if (RS && do_rs && (lane & 15) == 0) {   // every column of A*ones is the row sum: lanes of column 0 publish it
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = bm + wm * 64 + mi * 16 + (lane >> 4) * 4 + r;
+        const int row = bm + wm * WT + mi * 16 + (lane >> 4) * 4 + r;
         if (row < g.M) atomicAdd(g.rowsum + row, accr[mi][r]);
       }
   }
   // ---- epilogue: stage each wave's 64x64 fp32 tile through LDS (the 16x16 MFMA C/D
   // layout is col = lane&15, row = (lane>>4)*4 + r), then every lane owns 8
   // consecutive columns of a row: 16-B loads of bias/residual/aux and 16-B stores.
-  float* es = reinterpret_cast<float*>(smem) + wave * 64 * ES;
+  __syncthreads();   // every wave is done reading the last k-tile before the staging overwrites it
+  float* es = reinterpret_cast<float*>(smem) + wave * WT * ES;
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+  for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
+    for (int ni = 0; ni < MI; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r) es[(mi * 16 + (lane >> 4) * 4 + r) * ES + ni * 16 + (lane & 15)] = acc[mi][ni][r];
   __syncthreads();
@@ -328,24 +346,26 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
   T* aux = g.aux ? reinterpret_cast<T*>(g.aux) + coff : nullptr;
   if (slab) {
     // split-K partial: raw fp32 sums to this split's slab, one row per wave instruction
-    const int col = bn + wn * 64 + lane;
+    constexpr int RPI = 64 / WT;   // rows per wave instruction
+    const int cl = lane % WT, col = bn + wn * WT + cl;
     float* S = slab + ((long)(z * g.splitk + split) * g.M) * g.N;
 #pragma unroll 4
-    for (int rl = 0; rl < 64; ++rl) {
-      const int row = bm + wm * 64 + rl;
-      if (row < g.M && col < g.N) S[(long)row * g.N + col] = es[rl * ES + lane];
+    for (int rl = lane / WT; rl < WT; rl += RPI) {
+      const int row = bm + wm * WT + rl;
+      if (row < g.M && col < g.N) S[(long)row * g.N + col] = es[rl * ES + cl];
     }
     return;
   }
   if (g.atomic || g.c_f32) {
     // fp32 output (weight gradients): one row per wave instruction = 256 contiguous bytes
-    const int col = bn + wn * 64 + lane;
+    constexpr int RPI = 64 / WT;
+    const int cl = lane % WT, col = bn + wn * WT + cl;
     float* Cb = reinterpret_cast<float*>(g.c) + coff;
 #pragma unroll 4
-    for (int rl = 0; rl < 64; ++rl) {
-      const int row = bm + wm * 64 + rl;
+    for (int rl = lane / WT; rl < WT; rl += RPI) {
+      const int row = bm + wm * WT + rl;
       if (row >= g.M || col >= g.N) continue;
-      float v = es[rl * ES + lane];
+      float v = es[rl * ES + cl];
       if (bias) v += ldf<T>(bias + col);
       if (res) v += ldf<T>(res + (long)row * g.ldr + col);
       float* C = Cb + (long)row * g.ldc + col;
@@ -354,12 +374,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
     }
     return;
   }
-  const int c8 = (lane & 7) * 8;
-  const int col0 = bn + wn * 64 + c8;
+  constexpr int CPR = WT / 8, RPP = 64 / CPR;   // lanes per row (8 columns each), rows per pass
+  const int c8 = (lane % CPR) * 8;
+  const int col0 = bn + wn * WT + c8;
 #pragma unroll 1
-  for (int pass = 0; pass < 8; ++pass) {
-    const int rl = pass * 8 + (lane >> 3);
-    const int row = bm + wm * 64 + rl;
+  for (int pass = 0; pass < WT / RPP; ++pass) {
+    const int rl = pass * RPP + lane / CPR;
+    const int row = bm + wm * WT + rl;
     if (row >= g.M || col0 >= g.N) continue;
     float v[8];
     *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(es + rl * ES + c8);
@@ -414,18 +435,34 @@ bool view_vec(const dfk_view& v, int vec) {
   return true;
 }
 
-template <typename T, bool VECOK, bool CONV>
-void dispatch(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+template <typename T, int WT, bool VECOK, bool CONV>
+void dispatch_wt(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
   if (g.a_kmajor) {
     if (g.b_kmajor) {
-      if (g.rowsum) hipLaunchKernelGGL((gemm_kernel<T, true, true, VECOK, CONV, true>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
-      else hipLaunchKernelGGL((gemm_kernel<T, true, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+      if (g.rowsum) hipLaunchKernelGGL((gemm_kernel<T, WT, true, true, VECOK, CONV, true>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+      else hipLaunchKernelGGL((gemm_kernel<T, WT, true, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
     }
-    else hipLaunchKernelGGL((gemm_kernel<T, true, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_kernel<T, WT, true, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
   } else {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, false, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
-    else hipLaunchKernelGGL((gemm_kernel<T, false, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, WT, false, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_kernel<T, WT, false, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
   }
+}
+
+template <typename T, bool VECOK, bool CONV>
+void dispatch(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+  if (wt == 32) dispatch_wt<T, 32, VECOK, CONV>(g, grid, kchunk, evec, slab, s);
+  else dispatch_wt<T, 64, VECOK, CONV>(g, grid, kchunk, evec, slab, s);
+}
+
+// wave tile: 64 (128 x 128 workgroup tiles) unless that grid leaves the chip under one workgroup per CU
+// (or under two with a short K loop): then 32 (64 x 64 tiles, four times the workgroups, half the LDS,
+// a 4-deep register ring of k-tiles in flight)
+int pick_wt(const dfk_gemm_args& g) {
+  if (g.atomic || g.splitk > 1) return 64;   // caller-planned split-K grids (weight gradients)
+  const long tiles128 = (long)dfk_cdiv(g.N, 128) * dfk_cdiv(g.M, 128) * g.nz0 * g.nz1;
+  if (tiles128 < 256) return 32;
+  return tiles128 < 512 && g.K <= 1024 ? 32 : 64;
 }
 
 // automatic K split for grids that cannot fill the chip (caller asked for no split, no atomics)
@@ -433,7 +470,8 @@ template <typename T>
 int auto_splitk(const dfk_gemm_args& g) {
   constexpr int TBK = GT<T>::BK;
   if (g.atomic || g.splitk != 1 || g.M <= 0 || g.N <= 0) return 1;
-  const long tiles = (long)dfk_cdiv(g.N, BN) * dfk_cdiv(g.M, BM) * g.nz0 * g.nz1;
+  const int wt = pick_wt(g);
+  const long tiles = (long)dfk_cdiv(g.N, 2 * wt) * dfk_cdiv(g.M, 2 * wt) * g.nz0 * g.nz1;
   if (tiles >= 384) return 1;
   const int maxs = g.K / (2 * TBK);                 // at least two k-tiles per split
   const int want = (int)dfk_cdiv(768, tiles);
@@ -458,7 +496,8 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   if (autos > 1) gg.splitk = autos;
   int kchunk = dfk_cdiv(g.K, gg.splitk);
   kchunk = dfk_cdiv(kchunk, TBK) * TBK;
-  dim3 grid(dfk_cdiv(g.N, BN), dfk_cdiv(g.M, BM), g.nz0 * g.nz1 * gg.splitk);
+  const int wt = pick_wt(g);
+  dim3 grid(dfk_cdiv(g.N, 2 * wt), dfk_cdiv(g.M, 2 * wt), g.nz0 * g.nz1 * gg.splitk);
   if (grid.y > 65535 || grid.z > 65535) return DFK_EINVAL;
   // vector path also needs the contiguous extents to be whole vectors (else tails load element-wise)
   const bool vec = view_vec(g.a, VEC) && view_vec(g.b, VEC) && (g.a_kmajor ? g.M : g.K) % VEC == 0 &&
@@ -471,10 +510,10 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   const bool conv = g.a.conv_cg > 0 || g.b.conv_cg > 0;
   float* slab = autos > 1 ? reinterpret_cast<float*>(g.ws) : nullptr;
   if (vec) {
-    if (conv) dispatch<T, true, true>(gg, grid, kchunk, evec, slab, s);
-    else dispatch<T, true, false>(gg, grid, kchunk, evec, slab, s);
+    if (conv) dispatch<T, true, true>(gg, wt, grid, kchunk, evec, slab, s);
+    else dispatch<T, true, false>(gg, wt, grid, kchunk, evec, slab, s);
   } else {
-    dispatch<T, false, true>(gg, grid, kchunk, evec, slab, s);
+    dispatch<T, false, true>(gg, wt, grid, kchunk, evec, slab, s);
   }
   if (slab) {
     const long threads = (long)g.nz0 * g.nz1 * g.M * dfk_cdiv(g.N, 8);
