@@ -486,12 +486,14 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   if (!g.a.ptr || !g.b.ptr || !g.c) return DFK_EINVAL;
   if ((g.a.conv_cg > 0 && g.a.conv_stride <= 0) || (g.b.conv_cg > 0 && g.b.conv_stride <= 0)) return DFK_EINVAL;
   if (g.splitk < 1 || g.nz0 < 1 || g.nz1 < 1) return DFK_EINVAL;
-  if (g.splitk > 1 && !g.atomic) return DFK_EINVAL;
+  if (g.splitk > 1 && !g.atomic && !g.ws) return DFK_EINVAL;   // explicit split-K: fp32 slabs in ws
   if (g.atomic && (!g.c_f32 || g.bias || g.residual || g.act)) return DFK_EINVAL;
   if (g.act && g.act != 1 && !g.aux) return DFK_EINVAL;
   if (g.rowsum && (g.nz0 != 1 || g.nz1 != 1 || !g.a_kmajor || !g.b_kmajor)) return DFK_EINVAL;
   if (g.M <= 0 || g.N <= 0) return 0;
-  const int autos = g.ws ? auto_splitk<T>(g) : 1;
+  // split-K through fp32 slabs + a reduce/epilogue kernel: caller-chosen (splitk > 1, no atomics) or
+  // automatic for grids too small to fill the chip
+  const int autos = g.splitk > 1 && !g.atomic ? g.splitk : (g.ws ? auto_splitk<T>(g) : 1);
   dfk_gemm_args gg = g;
   if (autos > 1) gg.splitk = autos;
   int kchunk = dfk_cdiv(g.K, gg.splitk);
@@ -533,7 +535,8 @@ extern "C" int dfk_gemm(const dfk_gemm_args* g, hipStream_t s) {
 
 extern "C" int64_t dfk_gemm_workspace(const dfk_gemm_args* g) {
   if (!g) return -1;
-  const int autos = g->dtype == DFK_BF16 ? auto_splitk<bf16raw>(*g) : auto_splitk<float>(*g);
+  const int autos = g->splitk > 1 && !g->atomic ? g->splitk
+                    : (g->dtype == DFK_BF16 ? auto_splitk<bf16raw>(*g) : auto_splitk<float>(*g));
   if (autos <= 1) return 0;
   return (int64_t)autos * g->nz0 * g->nz1 * g->M * g->N * 4;
 }

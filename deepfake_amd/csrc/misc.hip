@@ -117,69 +117,91 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ grad
 
 // SwinV2 cosine attention prologue (swin_transformer2d.py:154-157): per (row, head)
 //   q' = q / max(|q|, 1e-12) * scale[h] ;  k' = k / max(|k|, 1e-12) ;  v' = v
-template <typename T>
-__global__ void cosine_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, const float* __restrict__ scale,
-                                  long rows, int heads, int hd) {
+// G = hd/8 consecutive lanes per (row, head), 8 elements (16 B) of q, k and v each; the norms reduce
+// across the lane group by xor shuffles.
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, int G>
+__global__ __launch_bounds__(256) void cosine_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+                                                         const float* __restrict__ scale, long rows, int heads) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= rows * heads) return;
-  const long r = idx / heads;
-  const int h = (int)(idx % heads);
-  const int C = heads * hd;
-  const T* q = qkv + r * 3 * C + h * hd;
-  T* o = out + r * 3 * C + h * hd;
+  const long grp = idx / G;
+  const int l = (int)(idx % G);
+  const bool ok = grp < rows * heads;
+  const long r = ok ? grp / heads : 0;
+  const int h = (int)(grp % heads);
+  const int C = heads * G * 8;
+  const long off = r * 3 * C + h * G * 8 + l * 8;
+  float q[8], k[8], v[8];
+  ld8<T>(qkv + off, q);
+  ld8<T>(qkv + off + C, k);
+  ld8<T>(qkv + off + 2 * C, v);
   float nq = 0.f, nk = 0.f;
-  for (int e = 0; e < hd; ++e) {
-    const float a = ldf<T>(q + e), b = ldf<T>(q + C + e);
-    nq += a * a;
-    nk += b * b;
-  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { nq += q[e] * q[e]; nk += k[e] * k[e]; }
+  nq = group_sum<G>(nq);
+  nk = group_sum<G>(nk);
   const float iq = scale[h] / fmaxf(sqrtf(nq), 1e-12f), ik = 1.f / fmaxf(sqrtf(nk), 1e-12f);
-  for (int e = 0; e < hd; ++e) {
-    stf<T>(o + e, ldf<T>(q + e) * iq);
-    stf<T>(o + C + e, ldf<T>(q + C + e) * ik);
-    o[2 * C + e] = q[2 * C + e];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { q[e] *= iq; k[e] *= ik; }
+  if (ok) {
+    st8<T>(out + off, q);
+    st8<T>(out + off + C, k);
+    st8<T>(out + off + 2 * C, v);
   }
 }
 
 // backward: dq = (s*dq' - qh*(qh . s*dq'))/|q| ; dk likewise (s = 1) ; dv = dv' ; dscale[h] += qh . dq'
-template <typename T>
-__global__ void cosine_bwd_kernel(const T* __restrict__ qkv, const T* __restrict__ dout, T* __restrict__ dqkv,
-                                  const float* __restrict__ scale, float* __restrict__ dscale, long rows, int heads,
-                                  int hd) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  float ds = 0.f;
-  int h = 0;
-  if (idx < rows * heads) {
-    const long r = idx / heads;
-    h = (int)(idx % heads);
-    const int C = heads * hd;
-    const long base = r * 3 * C + h * hd;
-#pragma unroll
-    for (int part = 0; part < 2; ++part) {
-      const T* x = qkv + base + part * C;
-      const T* d = dout + base + part * C;
-      T* dx = dqkv + base + part * C;
-      float n = 0.f;
-      for (int e = 0; e < hd; ++e) { const float a = ldf<T>(x + e); n += a * a; }
-      n = sqrtf(n);
-      const float inv = 1.f / fmaxf(n, 1e-12f);
-      const float s = part == 0 ? scale[h] : 1.f;
-      float dot = 0.f;  // xhat . dq'
-      for (int e = 0; e < hd; ++e) dot += ldf<T>(x + e) * inv * ldf<T>(d + e);
-      if (part == 0) ds = dot;
-      const bool clamped = n <= 1e-12f;
-      for (int e = 0; e < hd; ++e) {
-        const float xh = ldf<T>(x + e) * inv, g = s * ldf<T>(d + e);
-        stf<T>(dx + e, clamped ? g * inv : (g - xh * s * dot) * inv);
-      }
-    }
-    for (int e = 0; e < hd; ++e) dqkv[base + 2 * C + e] = dout[base + 2 * C + e];
-  }
-  // per-head reduction of ds: heads are interleaved along idx -> reduce through LDS by head
+template <typename T, int G>
+__global__ __launch_bounds__(256) void cosine_bwd_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                         T* __restrict__ dqkv, const float* __restrict__ scale,
+                                                         float* __restrict__ dscale, long rows, int heads) {
   __shared__ float red[64];
   if (threadIdx.x < 64) red[threadIdx.x] = 0.f;
   __syncthreads();
-  if (idx < rows * heads) atomicAdd(&red[h & 63], ds);
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long grp = idx / G;
+  const int l = (int)(idx % G);
+  const bool ok = grp < rows * heads;
+  const long r = ok ? grp / heads : 0;
+  const int h = (int)(grp % heads);
+  const int C = heads * G * 8;
+  const long base = r * 3 * C + h * G * 8 + l * 8;
+  float dsq = 0.f;
+#pragma unroll
+  for (int part = 0; part < 2; ++part) {
+    float x[8], d[8];
+    ld8<T>(qkv + base + part * C, x);
+    ld8<T>(dout + base + part * C, d);
+    float n2 = 0.f, xd = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { n2 += x[e] * x[e]; xd += x[e] * d[e]; }
+    n2 = group_sum<G>(n2);
+    xd = group_sum<G>(xd);
+    const float n = sqrtf(n2), inv = 1.f / fmaxf(n, 1e-12f);
+    const float sc = part == 0 ? scale[h] : 1.f;
+    const float dot = xd * inv;   // xhat . dq'
+    if (part == 0) dsq = dot;
+    const bool clamped = n <= 1e-12f;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float g = sc * d[e];
+      o[e] = clamped ? g * inv : (g - x[e] * inv * sc * dot) * inv;
+    }
+    if (ok) st8<T>(dqkv + base + part * C, o);
+  }
+  if (ok) {
+    float dv[8];
+    ld8<T>(dout + base + 2 * C, dv);
+    st8<T>(dqkv + base + 2 * C, dv);
+    if (l == 0) atomicAdd(&red[h & 63], dsq);
+  }
   __syncthreads();
   if (threadIdx.x < heads && threadIdx.x < 64 && red[threadIdx.x] != 0.f) atomicAdd(dscale + threadIdx.x, red[threadIdx.x]);
 }
@@ -188,32 +210,35 @@ __global__ void cosine_bwd_kernel(const T* __restrict__ qkv, const T* __restrict
 
 extern "C" int dfk_cosine_qk_fwd(const void* qkv, void* out, const float* scale, int64_t rows, int heads, int hd,
                                  int dtype, hipStream_t s) {
-  if (!qkv || !out || !scale || heads <= 0 || heads > 64) return DFK_EINVAL;
-  const long n = rows * heads;
+  if (!qkv || !out || !scale || heads <= 0 || heads > 64 || (hd != 32 && hd != 64)) return DFK_EINVAL;
+  if (reinterpret_cast<uintptr_t>(qkv) % 16 || reinterpret_cast<uintptr_t>(out) % 16) return DFK_EINVAL;
+  const long n = rows * heads * (hd / 8);
   if (n <= 0) return 0;
   const dim3 grid((unsigned)((n + 255) / 256));
-  if (dtype == DFK_BF16)
-    hipLaunchKernelGGL(cosine_fwd_kernel<bf16raw>, grid, dim3(256), 0, s, (const bf16raw*)qkv, (bf16raw*)out, scale,
-                       (long)rows, heads, hd);
-  else
-    hipLaunchKernelGGL(cosine_fwd_kernel<float>, grid, dim3(256), 0, s, (const float*)qkv, (float*)out, scale,
-                       (long)rows, heads, hd);
+#define COS_F(T, G) hipLaunchKernelGGL((cosine_fwd_kernel<T, G>), grid, dim3(256), 0, s, (const T*)qkv, (T*)out, scale, \
+                                       (long)rows, heads)
+  if (dtype == DFK_BF16) { if (hd == 32) COS_F(bf16raw, 4); else COS_F(bf16raw, 8); }
+  else { if (hd == 32) COS_F(float, 4); else COS_F(float, 8); }
+#undef COS_F
   DFK_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, const float* scale, float* dscale,
                                  int64_t rows, int heads, int hd, int dtype, hipStream_t s) {
-  if (!qkv || !dout || !dqkv || !scale || !dscale || heads <= 0 || heads > 64) return DFK_EINVAL;
-  const long n = rows * heads;
+  if (!qkv || !dout || !dqkv || !scale || !dscale || heads <= 0 || heads > 64 || (hd != 32 && hd != 64))
+    return DFK_EINVAL;
+  if (reinterpret_cast<uintptr_t>(qkv) % 16 || reinterpret_cast<uintptr_t>(dout) % 16 ||
+      reinterpret_cast<uintptr_t>(dqkv) % 16)
+    return DFK_EINVAL;
+  const long n = rows * heads * (hd / 8);
   if (n <= 0) return 0;
   const dim3 grid((unsigned)((n + 255) / 256));
-  if (dtype == DFK_BF16)
-    hipLaunchKernelGGL(cosine_bwd_kernel<bf16raw>, grid, dim3(256), 0, s, (const bf16raw*)qkv, (const bf16raw*)dout,
-                       (bf16raw*)dqkv, scale, dscale, (long)rows, heads, hd);
-  else
-    hipLaunchKernelGGL(cosine_bwd_kernel<float>, grid, dim3(256), 0, s, (const float*)qkv, (const float*)dout,
-                       (float*)dqkv, scale, dscale, (long)rows, heads, hd);
+#define COS_B(T, G) hipLaunchKernelGGL((cosine_bwd_kernel<T, G>), grid, dim3(256), 0, s, (const T*)qkv, (const T*)dout, \
+                                       (T*)dqkv, scale, dscale, (long)rows, heads)
+  if (dtype == DFK_BF16) { if (hd == 32) COS_B(bf16raw, 4); else COS_B(bf16raw, 8); }
+  else { if (hd == 32) COS_B(float, 4); else COS_B(float, 8); }
+#undef COS_B
   DFK_CHECK_LAUNCH();
   return 0;
 }

@@ -113,29 +113,51 @@ __global__ __launch_bounds__(256) void conv0_bwd_dw(const float* __restrict__ x,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                                     float eps, const T* __restrict__ dout, const float* __restrict__ red,
                                                     float* __restrict__ dw) {
+  // each workgroup sweeps a strided set of time blocks and keeps its dw partials in registers, so the
+  // 5120 dw entries take one atomic per workgroup (not one per 64-step block: same-address contention)
   __shared__ float xs[TB * KS + KW];
   __shared__ float ws[CH * KW];
-  const int b = blockIdx.y, t0 = blockIdx.x * TB;
-  stage(x, w, S, b, t0, xs, ws);
-  const int nt = min(TB, T0 - t0);
-  for (int c = threadIdx.x; c < CH; c += 256) {
+  const int b = blockIdx.y;
+  for (int i = threadIdx.x; i < CH * KW; i += 256) ws[i] = w[i];
+  constexpr int CPT = CH / 256;   // channels per thread
+  float acc[CPT][KW], m[CPT], r[CPT], g[CPT], be[CPT], A[CPT], Bm[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int c = threadIdx.x + j * 256;
     const float s = stats[((long)b * CH + c) * 2], q = stats[((long)b * CH + c) * 2 + 1];
-    const float m = s / T0, r = rsqrtf(fmaxf(q / T0 - m * m, 0.f) + eps);
-    const float g = gamma[c];
-    const float A = red[((long)b * CH + c) * 2] * g / T0, Bm = red[((long)b * CH + c) * 2 + 1] * g / T0;
-    float acc[KW];
+    m[j] = s / T0;
+    r[j] = rsqrtf(fmaxf(q / T0 - m[j] * m[j], 0.f) + eps);
+    g[j] = gamma[c];
+    be[j] = beta[c];
+    A[j] = red[((long)b * CH + c) * 2] * g[j] / T0;
+    Bm[j] = red[((long)b * CH + c) * 2 + 1] * g[j] / T0;
 #pragma unroll
-    for (int k = 0; k < KW; ++k) acc[k] = 0.f;
-    for (int tl = 0; tl < nt; ++tl) {
-      const float yh = (conv_at(xs, ws, tl, c) - m) * r;
-      const float dz = ldf<T>(dout + ((long)b * T0 + t0 + tl) * CH + c) * dgelu_f(yh * g + beta[c]);
-      const float dy = r * (g * dz - Bm - yh * A);
-#pragma unroll
-      for (int k = 0; k < KW; ++k) acc[k] += dy * xs[tl * KS + k];
-    }
-#pragma unroll
-    for (int k = 0; k < KW; ++k) atomicAdd(dw + c * KW + k, acc[k]);
+    for (int k = 0; k < KW; ++k) acc[j][k] = 0.f;
   }
+  const int ntb = (T0 + TB - 1) / TB;
+  for (int tb = blockIdx.x; tb < ntb; tb += gridDim.x) {
+    const int t0 = tb * TB;
+    __syncthreads();
+    const long base = (long)b * S + (long)t0 * KS;
+    for (int i = threadIdx.x; i < TB * KS + KW; i += 256) xs[i] = ((long)t0 * KS + i < S) ? x[base + i] : 0.f;
+    __syncthreads();
+    const int nt = min(TB, T0 - t0);
+    for (int tl = 0; tl < nt; ++tl) {
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        const int c = threadIdx.x + j * 256;
+        const float yh = (conv_at(xs, ws, tl, c) - m[j]) * r[j];
+        const float dz = ldf<T>(dout + ((long)b * T0 + t0 + tl) * CH + c) * dgelu_f(yh * g[j] + be[j]);
+        const float dy = r[j] * (g[j] * dz - Bm[j] - yh * A[j]);
+#pragma unroll
+        for (int k = 0; k < KW; ++k) acc[j][k] += dy * xs[tl * KS + k];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPT; ++j)
+#pragma unroll
+    for (int k = 0; k < KW; ++k) atomicAdd(dw + (threadIdx.x + j * 256) * KW + k, acc[j][k]);
 }
 
 // dgamma[c] += sum_b A[b,c] ; dbeta[c] += sum_b Bs[b,c]
@@ -173,16 +195,17 @@ extern "C" int dfk_w2v_conv0_bwd(const float* wave, int64_t B, int64_t S, const 
   if (!wave || !w || !gamma || !beta || !stats || !dout || !scratch || !dw || S < KW) return DFK_EINVAL;
   const int T0 = (int)((S - KW) / KS + 1);
   const dim3 grid(dfk_cdiv(T0, TB), (unsigned)B);
+  const dim3 gdw(std::min(dfk_cdiv(T0, TB), std::max(1, 256 / (int)B)), (unsigned)B);   // ~one workgroup per CU
   (void)hipMemsetAsync(scratch, 0, sizeof(float) * B * CH * 2, s);
   if (dtype == DFK_BF16) {
     hipLaunchKernelGGL(conv0_bwd_stats<bf16raw>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
                        (const bf16raw*)dout, scratch);
-    hipLaunchKernelGGL(conv0_bwd_dw<bf16raw>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
+    hipLaunchKernelGGL(conv0_bwd_dw<bf16raw>, gdw, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
                        (const bf16raw*)dout, scratch, dw);
   } else {
     hipLaunchKernelGGL(conv0_bwd_stats<float>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
                        (const float*)dout, scratch);
-    hipLaunchKernelGGL(conv0_bwd_dw<float>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
+    hipLaunchKernelGGL(conv0_bwd_dw<float>, gdw, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
                        (const float*)dout, scratch, dw);
   }
   if (dgamma || dbeta)

@@ -610,6 +610,14 @@ long tab_elems(const dfk_wattn_args& a, const Geo& g) {
   return (long)t.ncls * a.heads * t.per_ch;
 }
 
+// the window's shift class (table index): one bit per shifted dim, set for the last window along it
+__device__ __forceinline__ int win_class(const dfk_wattn_args& a, const Geo& g, int win) {
+  if (!g.use_mask) return 0;
+  const int wwi = win % g.nww, whi = (win / g.nww) % g.nwh, wdi = win / (g.nww * g.nwh);
+  return (a.sd > 0 && wdi == g.nwd - 1 ? 4 : 0) | (a.sh > 0 && whi == g.nwh - 1 ? 2 : 0) |
+         (a.sw > 0 && wwi == g.nww - 1 ? 1 : 0);
+}
+
 // Work order of the table kernels: units sorted by (shift class, head, clip, window) and dealt to the
 // XCDs in contiguous chunks (blocks b and b+8 share an XCD), so the workgroups that read one (class,
 // head) table run together on one XCD and the table is read from that XCD's L2.
@@ -878,7 +886,7 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     const long units = (long)a.B * g.nW * a.heads;
     if (units <= 0) return 0;
     const TabGeo tg = tab_geo(a, g);
-    const long nb = 0;   // the backward does not read the bwd layout yet
+    const long nb = tg.per_ch / 16;   // bwd layout too (read by dfk_wattn_bwd)
     float* tf = reinterpret_cast<float*>(a.tab);
     const long slots = tg.per_ch / 8 + (nb ? tg.per_ch / 16 : 0);
     hipLaunchKernelGGL(wattn_tab_kernel, dim3((unsigned)std::min<long>(dfk_cdiv(slots, 256), 64), tg.ncls * a.heads),
@@ -1275,10 +1283,13 @@ __global__ __launch_bounds__(256) void wattn_bwd_kernel(const dfk_wattn_bwd_args
 // from XOR-swizzled tiles, dS crossing the wave's scratch as dS^T (b64 stores,
 // tr16 loads), and a bank-swizzled dQ accumulator.
 
-template <int HD, bool RPB, bool MASK>
+// TAB: the score bias (RPB + shift mask, -inf beyond N) comes from the forward's bwd-layout table as the
+// C input of S = Q K^T (no per-score gather, label compare or key mask).
+template <int HD, bool RPB, bool MASK, bool TAB = false>
 __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(const dfk_wattn_bwd_args ba, const Geo g,
                                                                               int q0, int Qn, int accum_kv,
-                                                                              bf16raw* __restrict__ dsg) {
+                                                                              bf16raw* __restrict__ dsg,
+                                                                              const float* __restrict__ tabb) {
   // One workgroup = one (clip, window, head); wave w owns key blocks w, w + nwaves (dK, dV in registers).
   // All waves step through the query blocks together: per 32-query block each wave computes S, dP, P, dS
   // for its keys, accumulates dV += P^T dO and dK += dS^T Q, and its partial dQ = dS K; the partials are
@@ -1308,6 +1319,9 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
   const int win = unit % g.nW, b = unit / g.nW;
   const float* mrow = MASK ? a.mask + (((long)b * g.nW + win) % a.mask_nw) * g.N * g.N : nullptr;
   const int hoff = head * HD;
+  const f32x4* tch = TAB ? reinterpret_cast<const f32x4*>(tabb) +
+                               ((long)win_class(a, g, win) * a.heads + head) * (long)g.Np * g.Np / 4 + lane * 4
+                         : nullptr;
   const bf16raw* og = reinterpret_cast<const bf16raw*>(a.out);
   const bf16raw* dog = reinterpret_cast<const bf16raw*>(ba.dout);
   const bf16raw* qg = reinterpret_cast<const bf16raw*>(a.q);
@@ -1410,20 +1424,28 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
           }
         }
         float bias[2][2][4];
+        f32x4 tb[2][2];
+        if constexpr (TAB) {   // table tile (query block, key block): 4 x 16 B per lane
+          const f32x4* tp4 = tch + ((long)((q0 + qr0) / 32) * (g.Np / 32) + kb) * 256;
+#pragma unroll
+          for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) tb[qh][h2] = tp4[qh * 2 + h2];
+        }
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh)
 #pragma unroll
           for (int h2 = 0; h2 < 2; ++h2)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              bias[qh][h2][r] = RPB ? rpb2[(QP[qh][r] >> 5) - (kpk[h2] >> 5) + g.C0] : 0.f;
+              bias[qh][h2][r] = RPB && !TAB ? rpb2[(QP[qh][r] >> 5) - (kpk[h2] >> 5) + g.C0] : 0.f;
         // S = Q K^T, dP = dO V^T : rows = queries, lanes = keys
         f32x4 s[2][2], dp[2][2];
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh)
 #pragma unroll
           for (int h2 = 0; h2 < 2; ++h2) {
-            s[qh][h2] = f32x4{0, 0, 0, 0};
+            s[qh][h2] = TAB ? tb[qh][h2] : f32x4{0, 0, 0, 0};
             dp[qh][h2] = f32x4{0, 0, 0, 0};
 #pragma unroll
             for (int es = 0; es < HD / 32; ++es) {
@@ -1440,8 +1462,13 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
             float dsv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float x = s[qh][h2][r] * scale2 + (bias[qh][h2][r] + kneg[h2] - L2[qh][r]);
-              if (g.use_mask) x += ((QP[qh][r] ^ kpk[h2]) & 31) ? mpen : 0.f;
+              float x;
+              if constexpr (TAB) {
+                x = __builtin_fmaf(s[qh][h2][r], scale2, -L2[qh][r]);
+              } else {
+                x = s[qh][h2][r] * scale2 + (bias[qh][h2][r] + kneg[h2] - L2[qh][r]);
+                if (g.use_mask) x += ((QP[qh][r] ^ kpk[h2]) & 31) ? mpen : 0.f;
+              }
               if constexpr (MASK) {
                 const int q = q0 + qr0 + qh * 16 + grp * 4 + r, k = kb * 32 + h2 * 16 + ql;
                 if (q < g.N && k < g.N) x += mrow[q * g.N + k] * kLog2e;
@@ -1645,14 +1672,16 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
 #define LAUNCH_B16(HD, RPB, MASK)                                                                          \
   do {                                                                                                     \
     auto kfn = wattn_bwd_bf16_kernel<HD, RPB, MASK>;                                                       \
+    auto kft = wattn_bwd_bf16_kernel<HD, RPB, false, true>;                                                \
     static bool attr_set = false;                                                                          \
     if (!attr_set) {                                                                                       \
       (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      (void)hipFuncSetAttribute((const void*)kft, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
       attr_set = true;                                                                                     \
     }                                                                                                      \
     for (int q0 = 0; q0 < g.Np; q0 += Qn)                                                                  \
-      hipLaunchKernelGGL(kfn, dim3((unsigned)units), dim3(64 * nwaves), lds, s, *bp, g, q0,                \
-                         std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0, dsg);                                    \
+      hipLaunchKernelGGL(tabb ? kft : kfn, dim3((unsigned)units), dim3(64 * nwaves), lds, s, *bp, g, q0,   \
+                         std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0, dsg, tabb);                              \
   } while (0)
 #define PICK_B16(HD)                                                 \
   do {                                                               \
@@ -1663,6 +1692,9 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     if (want_drpb && !bp->ws) return DFK_EINVAL;  // dRPB needs the dfk_wattn_bwd_workspace scratch
     const DsPlan pl = ds_plan(a, g);
     bf16raw* dsg = want_drpb ? reinterpret_cast<bf16raw*>(bp->ws) : nullptr;
+    // the forward left both table layouts in a.tab (same args, same rpb): the bwd layout follows the fwd one
+    const float* tabb = a.tab && !a.mask && a.scale > 0.f ? reinterpret_cast<const float*>(a.tab) + tab_elems(a, g)
+                                                          : nullptr;
     if (a.hd == 32) PICK_B16(32); else PICK_B16(64);
 #undef PICK_B16
 #undef LAUNCH_B16

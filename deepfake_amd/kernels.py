@@ -88,10 +88,15 @@ def splitk_for(tiles, K, min_k=256):
 
 
 def linear_dw(dy, x, dw, db=None):
-    """dw[N,K] (fp32, +=) += dy[M,N]^T @ x[M,K]  (split over M, fp32 atomics); with db [N] fp32:
-    db += column sums of dy (the bias gradient) from the same pass over dy."""
+    """dw[N,K] (fp32, +=) += dy[M,N]^T @ x[M,K]; with db [N] fp32: db += column sums of dy (the bias
+    gradient) from the same pass over dy.  Output grids that fill the chip run unsplit and add in the
+    epilogue; skinny ones split the M reduction and add fp32 partials atomically."""
     M, N = dy.shape
     K = x.shape[1]
+    if math.ceil(N / 64) * math.ceil(K / 64) >= 256:
+        gemm(dy, dy.stride(0), True, x, x.stride(0), True, N, K, M, dw, dw.stride(0), dtype=L.dt(dy), c_f32=True,
+             beta=1.0, rowsum=db)
+        return dw
     tiles = math.ceil(N / 128) * math.ceil(K / 128)
     gemm(dy, dy.stride(0), True, x, x.stride(0), True, N, K, M, dw, dw.stride(0), dtype=L.dt(dy), c_f32=True,
          atomic=True, splitk=splitk_for(tiles, M), rowsum=db)

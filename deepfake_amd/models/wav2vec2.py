@@ -119,9 +119,17 @@ class Wav2Vec2PositionalConvEmbedding(nn.Module):
         if config.num_conv_pos_embeddings % 2:
             raise NotImplementedError("odd num_conv_pos_embeddings")
 
+    def weight(self):
+        """weight_norm(dim=2): g * v / ||v|| with the norm over dims (0, 1) — same parameters and state_dict
+        keys as the parametrization, composed from plain reductions (torch's dim=2 weight-norm kernels take
+        ~0.45 ms each way on this [768, 48, 128] shape)."""
+        p = self.conv.parametrizations.weight
+        g, v = p.original0, p.original1
+        return v * (g / v.pow(2).sum(dim=(0, 1), keepdim=True).sqrt())
+
     def add_to(self, x):
         """x + pos_conv(x) fused (HF/:689-690)."""
-        return Fn.PosConvFn.apply(x, self.conv.weight, self.conv.bias, self.groups)
+        return Fn.PosConvFn.apply(x, self.weight(), self.conv.bias, self.groups)
 
 
 class Wav2Vec2Attention(nn.Module):

@@ -68,12 +68,14 @@ def test_wattn_fwd(dt, case):
     assert err < (2e-2 if dt == torch.bfloat16 else 1e-5), err
 
 
+@pytest.mark.parametrize("table", [True, False], ids=["tab", "notab"])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
-def test_wattn_bwd(dt, case):
+def test_wattn_bwd(dt, case, table):
+    """bf16: with the forward's bias tables (table-driven kernels) and without (gather kernels)."""
     dims, window, fw, shift, heads, hd = case
-    if False:
-        pytest.skip("fp32 (parity-mode) backward keeps the window in LDS: N <= 256 (C1 sizes)")
+    if dt == torch.float32 and not table:
+        pytest.skip("fp32 parity mode has one kernel pair")
     g = torch.Generator(device=DEV).manual_seed(4)
     rows = dims[0] * dims[1] * dims[2] * dims[3]
     C = heads * hd
@@ -82,14 +84,15 @@ def test_wattn_bwd(dt, case):
     Lt = (2 * fw[0] - 1) * (2 * fw[1] - 1) * (2 * fw[2] - 1)
     rpb = torch.randn(Lt, heads, device=DEV, generator=g) * 0.5 if hd == 32 else None
     scale = hd ** -0.5
-    out, lse = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, window, fw, shift, heads, hd, scale,
-                           rpb=rpb, pads=pads)
+    out, lse, tab = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, window, fw, shift, heads, hd, scale,
+                                rpb=rpb, pads=pads, use_table=table, return_table=True)
+    assert (tab is not None) == (table and dt == torch.bfloat16)
     dout = torch.randn(rows, C, device=DEV, generator=g).to(dt)
     dqkv = torch.empty_like(qkv)
     drpb = torch.zeros(Lt, heads, device=DEV) if rpb is not None else None
     dpads = [torch.zeros(C, device=DEV) for _ in range(3)]
     K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, 3 * C, dims, window, fw, shift, heads, hd, scale, rpb,
-                 pads), dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C, drpb=drpb, dpads=dpads)
+                 pads), dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C, drpb=drpb, dpads=dpads, tab=tab)
     # reference
     qr = qkv.float().requires_grad_(True)
     pr = [p.float().requires_grad_(True) for p in pads]

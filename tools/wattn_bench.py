@@ -50,8 +50,8 @@ def main():
             nW *= -(-n // w)
         scale = hd ** -0.5
         out = torch.empty(rows, C, device="cuda", dtype=dt)
-        _, lse = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, win, fw, shift, heads, hd, scale, rpb=rpb,
-                             out=out)
+        _, lse, tab = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, win, fw, shift, heads, hd, scale,
+                                  rpb=rpb, out=out, return_table=True)
         dout = torch.randn(rows, C, device="cuda").to(dt)
         dqkv = torch.empty_like(qkv)
         drpb = torch.zeros_like(rpb) if rpb is not None else None
@@ -59,7 +59,7 @@ def main():
                                        rpb=rpb, out=out))
         tb = timed(lambda: K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, 3 * C, dims, win, fw, shift, heads,
                                         hd, scale, rpb, None), dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C,
-                                       drpb=drpb))
+                                       drpb=drpb, tab=tab))
         units = dims[0] * nW * heads
         ff = 4.0 * units * N * N * hd
         fb = 10.0 * units * N * N * hd
