@@ -70,6 +70,7 @@ SIGNATURES = {
     "dfk_wattn_bwd": [C.POINTER(WattnBwdArgs), _VP],
     "dfk_wattn_bwd_workspace": [C.POINTER(WattnArgs)],
     "dfk_wattn_table_workspace": [C.POINTER(WattnArgs)],
+    "dfk_wattn_table": [C.POINTER(WattnArgs), _VP],
     "dfk_patch_im2col": [_VP, C.c_int, _VP, C.c_int, C.POINTER(Im2colArgs), _VP],
     "dfk_patch_merge": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],
     "dfk_rowmean": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],

@@ -23,6 +23,61 @@ __global__ void im2col_kernel(const TI* __restrict__ x, TO* __restrict__ out, df
   stf<TO>(out + idx, v);
 }
 
+// Row-staged im2col for fp32 input with unit W stride and 16-B aligned rows (the clip / mel-image
+// PatchEmbed inputs): one workgroup per output row of tokens (b, d, h).  The cin*pd*ph input rows those
+// tokens cover are staged into LDS with coalesced 16-B loads (zero beyond T / H / W), then every lane
+// writes 16-B chunks of the token-major [Wo][K] output, so both HBM streams move whole lines.
+template <typename TO>
+__global__ __launch_bounds__(256) void im2col_rows_kernel(const float* __restrict__ x, TO* __restrict__ out,
+                                                          dfk_im2col_args a) {
+  extern __shared__ __attribute__((aligned(16))) float slab[];   // [cin*pd*ph][Ws]
+  const int Wp = a.Wo * a.pw, Ws = Wp + 4;   // +4 floats: a token's rows spread over the banks
+  long r = blockIdx.x;
+  const int h = (int)(r % a.Ho);
+  r /= a.Ho;
+  const int d = (int)(r % a.Do);
+  const long b = r / a.Do;
+  const int nrows = a.cin * a.pd * a.ph, q4 = Wp / 4;
+  for (int i = threadIdx.x; i < nrows * q4; i += blockDim.x) {
+    const int sr = i / q4, x0 = (i - sr * q4) * 4;
+    const int c = sr / (a.pd * a.ph), kd = (sr / a.ph) % a.pd, kh = sr % a.ph;
+    const int t = d * a.pd + kd, y = h * a.ph + kh;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < a.T && y < a.H) {
+      const float* p = x + b * a.sb + c * a.sc + (long)t * a.st + (long)y * a.sh + x0;
+      if (x0 + 4 <= a.W) {
+        v = *reinterpret_cast<const float4*>(p);
+      } else {
+        float e[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 4; ++j)
+          if (x0 + j < a.W) e[j] = p[j];
+        v = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+    *reinterpret_cast<float4*>(slab + sr * Ws + x0) = v;
+  }
+  __syncthreads();
+  const int K = nrows * a.pw, kc = K / 8;
+  TO* o = out + (long)blockIdx.x * a.Wo * K;
+  for (int j = threadIdx.x; j < a.Wo * kc; j += blockDim.x) {
+    const int w = j / kc, k0 = (j - w * kc) * 8;
+    float v[8];
+    if (a.pw == 4) {   // the chunk is 4 columns of two consecutive staged rows: two 16-B LDS reads
+      const int sr = k0 / 4;
+      const float4 lo = *reinterpret_cast<const float4*>(slab + sr * Ws + w * 4);
+      const float4 hi = *reinterpret_cast<const float4*>(slab + (sr + 1) * Ws + w * 4);
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = k0 + e, sr = k / a.pw;
+        v[e] = slab[sr * Ws + w * a.pw + (k - sr * a.pw)];
+      }
+    }
+    st8<TO>(o + (long)w * K + k0, v);
+  }
+}
+
 // PatchMerging (video_swin_transformer.py:300-311 / swin_transformer2d.py:349-358):
 // out[(b,d,h2,w2)][q*C + c] = x[b,d,2h2+i,2w2+j,c], (i,j) = (0,0),(1,0),(0,1),(1,1) for q = 0..3
 template <typename T>
@@ -249,6 +304,23 @@ extern "C" int dfk_patch_im2col(const void* x, int x_dtype, void* out, int out_d
   const long rows = (long)a->B * a->Do * a->Ho * a->Wo;
   const long total = rows * a->cin * a->pd * a->ph * a->pw;
   if (total <= 0) return 0;
+  {
+    const int K = a->cin * a->pd * a->ph * a->pw, Wp = a->Wo * a->pw;
+    const size_t slab = (size_t)a->cin * a->pd * a->ph * (Wp + 4) * sizeof(float);
+    const bool rows_ok = x_dtype == DFK_F32 && a->sw == 1 && a->sb % 4 == 0 && a->sc % 4 == 0 && a->st % 4 == 0 &&
+                         a->sh % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                         (reinterpret_cast<uintptr_t>(out) & 15) == 0 && Wp % 4 == 0 && K % 8 == 0 &&
+                         slab <= 64 * 1024 && (out_dtype == DFK_BF16 || out_dtype == DFK_F32);
+    if (rows_ok) {
+      const dim3 g((unsigned)((long)a->B * a->Do * a->Ho));
+      if (out_dtype == DFK_BF16)
+        hipLaunchKernelGGL(im2col_rows_kernel<bf16raw>, g, dim3(256), slab, s, (const float*)x, (bf16raw*)out, *a);
+      else
+        hipLaunchKernelGGL(im2col_rows_kernel<float>, g, dim3(256), slab, s, (const float*)x, (float*)out, *a);
+      DFK_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   const dim3 grid((unsigned)((total + 255) / 256));
   if (x_dtype == DFK_F32 && out_dtype == DFK_BF16)
     hipLaunchKernelGGL((im2col_kernel<float, bf16raw>), grid, dim3(256), 0, s, (const float*)x, (bf16raw*)out, *a, total);

@@ -878,19 +878,28 @@ size_t fwd_lds(const dfk_wattn_args& a, const Geo& g) {
 
 }  // namespace
 
+extern "C" int dfk_wattn_table(const dfk_wattn_args* ap, hipStream_t s) {
+  if (!ap || !args_ok(*ap) || !ap->tab || ap->dtype != DFK_BF16 || ap->mask || !(ap->scale > 0.f)) return DFK_EINVAL;
+  const dfk_wattn_args& a = *ap;
+  const Geo g = make_geo(a);
+  const TabGeo tg = tab_geo(a, g);
+  float* tf = reinterpret_cast<float*>(a.tab);
+  const long slots = tg.per_ch / 8 + tg.per_ch / 16;   // fwd + bwd layouts
+  hipLaunchKernelGGL(wattn_tab_kernel, dim3((unsigned)std::min<long>(dfk_cdiv(slots, 256), 64), tg.ncls * a.heads),
+                     dim3(256), 4 * (size_t)(g.Np + g.L), s, a, g, tg.per_ch / 8, tg.per_ch / 16, tf,
+                     tf + tab_elems(a, g));
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
   if (!ap || !args_ok(*ap)) return DFK_EINVAL;
   const dfk_wattn_args& a = *ap;
   const Geo g = make_geo(a);
-  if (a.dtype == DFK_BF16 && a.tab && !a.mask && a.scale > 0.f) {
+  if (a.dtype == DFK_BF16 && a.tab && !a.mask && a.scale > 0.f) {   // table built by dfk_wattn_table
     const long units = (long)a.B * g.nW * a.heads;
     if (units <= 0) return 0;
-    const TabGeo tg = tab_geo(a, g);
-    const long nb = tg.per_ch / 16;   // bwd layout too (read by dfk_wattn_bwd)
-    float* tf = reinterpret_cast<float*>(a.tab);
-    const long slots = tg.per_ch / 8 + (nb ? tg.per_ch / 16 : 0);
-    hipLaunchKernelGGL(wattn_tab_kernel, dim3((unsigned)std::min<long>(dfk_cdiv(slots, 256), 64), tg.ncls * a.heads),
-                       dim3(256), 4 * (size_t)(g.Np + g.L), s, a, g, tg.per_ch / 8, nb, tf, tf + tab_elems(a, g));
+    const float* tf = reinterpret_cast<const float*>(a.tab);
     const size_t lds = 4 * (size_t)g.Np * a.hd;
     const int nqb = g.Np / 32;
     const int nw = std::min(4, nqb);

@@ -162,24 +162,26 @@ def window_geometry(dims, window):
 
 
 def wattn_fwd(q, k, v, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb=None, pads=None,
-              out=None, need_lse=True, mask=None, use_table=True, return_table=False):
+              out=None, need_lse=True, mask=None, use_table=True, return_table=False, tab=None):
     """Token-major window attention core; returns (out [rows, heads*hd], lse[, tab]).
-    use_table: bf16 score-bias tables (RPB + shift mask per shift class, dfk_wattn_table_workspace);
-    the backward must be handed the same `tab`."""
+    use_table: bf16 score-bias tables (RPB + shift mask per shift class, built by dfk_wattn_table, or
+    `tab` from an earlier call with the same geometry and rpb); the backward must get the same `tab`."""
     rows = dims[0] * dims[1] * dims[2] * dims[3]
     if out is None:
         out = torch.empty(rows, heads * hd, device=q.device, dtype=q.dtype)
     nW, N, Np = window_geometry(dims, window)
     lse = torch.empty(dims[0] * nW * heads, Np, device=q.device, dtype=torch.float32) if need_lse else None
     a = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse, mask)
-    tab = None
-    if use_table and os.environ.get("DFK_WATTN_TABLE", "1") != "0":
+    if tab is not None:
+        a.tab = tab.data_ptr()
+    elif use_table and os.environ.get("DFK_WATTN_TABLE", "1") != "0":
         nbytes = L.lib().dfk_wattn_table_workspace(a)
         if nbytes < 0:
             raise RuntimeError("dfk_wattn_table_workspace: invalid arguments")
         if nbytes > 0:
             tab = torch.empty(nbytes // 4, device=q.device, dtype=torch.float32)
             a.tab = tab.data_ptr()
+            L.check(L.lib().dfk_wattn_table(a, L.stream()), "wattn_table")
     L.check(L.lib().dfk_wattn_fwd(a, L.stream()), "wattn_fwd")
     if return_table:
         return out, lse, tab

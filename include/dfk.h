@@ -113,10 +113,10 @@ int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float*
  *   scale multiplies q before q k^T (Q5).
  *   lse (fp32 [B*nW, nH, Np]) saved for the backward.
  *   tab: bf16 path only (NULL = table-free kernels): device scratch of
- *   dfk_wattn_table_workspace() bytes.  dfk_wattn_fwd writes the per-(shift
- *   class, head) score-bias tables there (RPB + shift mask, fp16, in MFMA
- *   accumulator order); dfk_wattn_bwd reads them, so the backward must get the
- *   same buffer, untouched, with the same rpb. */
+ *   dfk_wattn_table_workspace() bytes holding the per-(shift class, head)
+ *   score-bias tables (RPB + shift mask, fp32, in MFMA accumulator order) that
+ *   dfk_wattn_table builds from rpb; dfk_wattn_fwd and dfk_wattn_bwd read them,
+ *   so both must get the buffer built with the same geometry and rpb. */
 typedef struct {
   const void* q; const void* k; const void* v;
   void* out;
@@ -137,6 +137,9 @@ typedef struct {
 } dfk_wattn_args;
 int dfk_wattn_fwd(const dfk_wattn_args* a, hipStream_t stream);
 int64_t dfk_wattn_table_workspace(const dfk_wattn_args* a);
+/* builds a->tab (fwd and bwd layouts) from a->rpb, the shift and the window geometry
+ * (replaces the RPB gather + mask add of WindowAttention3D.forward, :152-163) */
+int dfk_wattn_table(const dfk_wattn_args* a, hipStream_t stream);
 /* backward: f is the forward's argument block (f.out = the forward output O,
  * f.lse its log-sum-exp).  dq/dk/dv are written (=) at the q/k/v layout with
  * row stride ld_dqkv; drpb [L,nH] fp32 (+=); gradients of padded positions
