@@ -65,7 +65,8 @@ SIGNATURES = {
     "dfk_gemm_workspace": [C.POINTER(GemmArgs)],
     "dfk_colsum": [_VP, C.c_int, _I64, _I64, _I64, _VP, _VP],
     "dfk_layernorm_fwd": [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, _F, C.c_int, _VP],
-    "dfk_layernorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, C.c_int, C.c_int, _VP],
+    "dfk_layernorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, C.c_int, C.c_int, _VP, _VP],
+    "dfk_layernorm_bwd_workspace": [_I64, _I32],
     "dfk_wattn_fwd": [C.POINTER(WattnArgs), _VP],
     "dfk_wattn_bwd": [C.POINTER(WattnBwdArgs), _VP],
     "dfk_wattn_bwd_workspace": [C.POINTER(WattnArgs)],
@@ -84,7 +85,7 @@ SIGNATURES = {
 }
 
 _lib = None
-RESTYPES = {"dfk_wattn_bwd_workspace": _I64, "dfk_wattn_table_workspace": _I64, "dfk_gemm_workspace": _I64}
+RESTYPES = {"dfk_layernorm_bwd_workspace": _I64, "dfk_wattn_bwd_workspace": _I64, "dfk_wattn_table_workspace": _I64, "dfk_gemm_workspace": _I64}
 
 
 def lib():

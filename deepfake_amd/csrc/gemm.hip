@@ -460,6 +460,8 @@ void dispatch(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, f
 // a 4-deep register ring of k-tiles in flight)
 int pick_wt(const dfk_gemm_args& g) {
   if (g.atomic || g.splitk > 1) return 64;   // caller-planned split-K grids (weight gradients)
+  static const int force = getenv("DFK_GEMM_WT") ? atoi(getenv("DFK_GEMM_WT")) : 0;   // tuning runs only
+  if (force == 32 || force == 64) return force;
   const long tiles128 = (long)dfk_cdiv(g.N, 128) * dfk_cdiv(g.M, 128) * g.nz0 * g.nz1;
   if (tiles128 < 256) return 32;
   return tiles128 < 512 && g.K <= 1024 ? 32 : 64;

@@ -102,7 +102,7 @@ template <typename T, int L, int V>
 __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T* __restrict__ x,
                                               const T* __restrict__ w, const float* __restrict__ mean,
                                               const float* __restrict__ rstd, T* __restrict__ dx, float* dw,
-                                              float* db, long rows, int C, int accumulate) {
+                                              float* db, long rows, int C, int accumulate, float* __restrict__ part) {
   constexpr int RPW = 64 / L;
   constexpr bool KEEP = V <= 4;   // x, dy stay in registers between the two sweeps
   extern __shared__ float red[];  // [2][C] block partials of dw, db
@@ -192,10 +192,31 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
     }
     __syncthreads();
   }
+  if (part) {   // block partials -> [blocks][2C] slab, summed by a column-sum pass (no same-address atomics)
+    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) part[(long)blockIdx.x * 2 * C + i] = red[i];
+    return;
+  }
   for (int i = threadIdx.x; i < C; i += blockDim.x) {
     if (dw) atomicAdd(dw + i, red[i]);
     if (db) atomicAdd(db + i, red[C + i]);
   }
+}
+
+// out[j] += sum over the slab rows of part[r][col0 + j]  (64-row chunks, one atomic per chunk and column)
+__global__ __launch_bounds__(256) void slab_colsum(const float* __restrict__ part, int rows, int ld, int col0, int cols,
+                                                   float* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cols || !out) return;
+  const int r0 = blockIdx.y * 64, r1 = min(rows, r0 + 64);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += part[(long)r * ld + col0 + j];
+  atomicAdd(out + j, s);
+}
+
+long bwd_blocks(long rows, int C) {
+  const int nv = C / 8;
+  const int L = nv <= 16 ? 16 : (nv <= 32 ? 32 : 64);
+  return std::min<long>(2048, dfk_cdiv(rows, 4L * (64 / L)));
 }
 
 template <typename T, int L, int V>
@@ -208,11 +229,16 @@ void fwd_launch(const void* x, const void* w, const void* b, void* y, float* mea
 
 template <typename T, int L, int V>
 void bwd_launch(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx, float* dw,
-                float* db, long rows, int C, int accumulate, hipStream_t s) {
-  const long per_block = 4L * (64 / L);
-  const int blocks = (int)std::min<long>(2048, dfk_cdiv(rows, per_block));
+                float* db, long rows, int C, int accumulate, float* ws, hipStream_t s) {
+  const int blocks = (int)bwd_blocks(rows, C);
+  float* part = ws && (dw || db) ? ws : nullptr;
   hipLaunchKernelGGL((ln_bwd<T, L, V>), dim3(blocks), dim3(256), 2 * C * sizeof(float), s, (const T*)dy,
-                     (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate);
+                     (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part);
+  if (part) {
+    const dim3 g(dfk_cdiv(C, 256), dfk_cdiv(blocks, 64));
+    hipLaunchKernelGGL(slab_colsum, g, dim3(256), 0, s, part, blocks, 2 * C, 0, C, dw);
+    hipLaunchKernelGGL(slab_colsum, g, dim3(256), 0, s, part, blocks, 2 * C, C, C, db);
+  }
 }
 
 // (L, V) for C: L = lanes per row, V = 8-channel vectors per lane
@@ -245,8 +271,8 @@ struct Fwd {
 template <typename T, int L, int V>
 struct Bwd {
   static void run(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
-                  float* dw, float* db, long rows, int C, int accumulate, hipStream_t s) {
-    bwd_launch<T, L, V>(dy, x, w, mean, rstd, dx, dw, db, rows, C, accumulate, s);
+                  float* dw, float* db, long rows, int C, int accumulate, float* ws, hipStream_t s) {
+    bwd_launch<T, L, V>(dy, x, w, mean, rstd, dx, dw, db, rows, C, accumulate, ws, s);
   }
 };
 
@@ -263,14 +289,19 @@ extern "C" int dfk_layernorm_fwd(const void* x, const void* w, const void* b, vo
   return 0;
 }
 
+extern "C" int64_t dfk_layernorm_bwd_workspace(int64_t rows, int32_t C) {
+  if (rows <= 0 || C <= 0) return 0;
+  return bwd_blocks(rows, C) * 2 * (int64_t)C * (int64_t)sizeof(float);
+}
+
 extern "C" int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                                  void* dx, float* dw, float* db, int64_t rows, int32_t C, int accumulate, int dtype,
-                                 hipStream_t s) {
+                                 float* ws, hipStream_t s) {
   if (!dy || !x || !w || !mean || !rstd || !dx || C <= 0 || C % 8 || C > 4096) return DFK_EINVAL;
   if (rows <= 0) return 0;
   const bool ok = dtype == DFK_BF16
-                      ? pick<bf16raw, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, s)
-                      : pick<float, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, s);
+                      ? pick<bf16raw, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, ws, s)
+                      : pick<float, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, ws, s);
   if (!ok) return DFK_EINVAL;
   DFK_CHECK_LAUNCH();
   return 0;

@@ -121,13 +121,17 @@ def layernorm_fwd(x, w, b, eps=1e-5, out=None):
     return out, mean, rstd
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False):
+def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False, slab_partials=False):
     rows, C = x.shape
     if dx is None:
         dx = torch.empty_like(x)
+    ws = None
+    if slab_partials and (dw is not None or db is not None):   # per-workgroup dw/db partials + column sums
+        ws = torch.empty(max(L.lib().dfk_layernorm_bwd_workspace(rows, C) // 4, 1), device=x.device,
+                         dtype=torch.float32)
     L.check(L.lib().dfk_layernorm_bwd(L.ptr(dy), L.ptr(x), L.ptr(w), L.ptr(mean), L.ptr(rstd), L.ptr(dx),
-                                      L.ptr(dw), L.ptr(db), rows, C, int(accumulate), L.dt(x), L.stream()),
-            "layernorm_bwd")
+                                      L.ptr(dw), L.ptr(db), rows, C, int(accumulate), L.dt(x), L.ptr(ws),
+                                      L.stream()), "layernorm_bwd")
     return dx
 
 

@@ -91,10 +91,14 @@ int dfk_colsum(const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld,
  * y = (x-mean)*rstd*w + b; saves mean/rstd (fp32) for the backward. */
 int dfk_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
                       int64_t rows, int32_t C, float eps, int dtype, hipStream_t stream);
-/* dx (=, or += when accumulate) ; dw, db accumulate (fp32 atomics). */
+/* dx (=, or += when accumulate) ; dw, db accumulate (+=).  ws: fp32 scratch of
+ * dfk_layernorm_bwd_workspace(rows, C) bytes for per-workgroup dw/db partials,
+ * column-summed by a second pass; NULL: fp32 atomics per workgroup and channel
+ * (same-address contention: slow when many workgroups share few channels). */
 int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                       void* dx, float* dw, float* db, int64_t rows, int32_t C, int accumulate, int dtype,
-                      hipStream_t stream);
+                      float* ws, hipStream_t stream);
+int64_t dfk_layernorm_bwd_workspace(int64_t rows, int32_t C);
 
 /* Windowed multi-head attention core on token-major buffers (no window
  * partition / roll copies: both are index arithmetic inside the kernel).

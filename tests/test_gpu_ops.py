@@ -76,3 +76,9 @@ def test_layernorm(dt, rows, C):
     assert rel(dx, xr.grad) < tol(dt) * 2
     assert rel(dw, wr.grad) < tol(dt)
     assert rel(db, br.grad) < tol(dt)
+    # dw/db through per-workgroup partials + column sums instead of atomics
+    dw2 = torch.zeros(C, device=DEV)
+    db2 = torch.zeros(C, device=DEV)
+    K.layernorm_bwd(dy, x, w, mean, rstd, dw2, db2, slab_partials=True)
+    assert rel(dw2, wr.grad) < tol(dt)
+    assert rel(db2, br.grad) < tol(dt)
