@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "../../include/dfk.h"
 
 typedef uint16_t bf16raw;  // bf16 storage (upper half of an fp32)

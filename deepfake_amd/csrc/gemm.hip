@@ -455,16 +455,17 @@ void dispatch(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, f
   else dispatch_wt<T, 64, VECOK, CONV>(g, grid, kchunk, evec, slab, s);
 }
 
-// wave tile: 64 (128 x 128 workgroup tiles) unless that grid leaves the chip under one workgroup per CU
-// (or under two with a short K loop): then 32 (64 x 64 tiles, four times the workgroups, half the LDS,
-// a 4-deep register ring of k-tiles in flight)
+// wave tile: 64 (128 x 128 workgroup tiles) unless that grid has fewer than eight tiles per CU: then 32
+// (64 x 64 tiles, four times the workgroups, half the LDS, a 4-deep register ring of k-tiles in flight)
 int pick_wt(const dfk_gemm_args& g) {
   if (g.atomic || g.splitk > 1) return 64;   // caller-planned split-K grids (weight gradients)
   static const int force = getenv("DFK_GEMM_WT") ? atoi(getenv("DFK_GEMM_WT")) : 0;   // tuning runs only
   if (force == 32 || force == 64) return force;
+  // measured on the C2 Linear shapes (tools/gemm_bench.py, both tile shapes): below 2048 128x128 tiles (eight
+  // per CU) the 64x64 tiles with the k-tile ring win or tie at every K (e.g. [25088,1536]x[1536,384] 98 -> 73
+  // us, [6272,3072]x[3072,768] 86 -> 77 us), above it the 128x128 tiles win
   const long tiles128 = (long)dfk_cdiv(g.N, 128) * dfk_cdiv(g.M, 128) * g.nz0 * g.nz1;
-  if (tiles128 < 256) return 32;
-  return tiles128 < 512 && g.K <= 1024 ? 32 : 64;
+  return tiles128 < 2048 ? 32 : 64;
 }
 
 // automatic K split for grids that cannot fill the chip (caller asked for no split, no atomics)

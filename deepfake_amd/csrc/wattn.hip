@@ -32,7 +32,12 @@ struct Geo {
   int L;                   // rpb table rows
   int C0;                  // rpb index offset
   int use_mask;
+  uint32_t m_hw, m_w;      // fast-division multipliers for wh*ww and ww (0: divisor 1), exact for i < 2^16
 };
+
+// floor(x / n) for x < 2^16, n < 2^16 with m = floor((2^32-1)/n) + 1 (m = 0 encodes n = 1): the error of
+// x*m/2^32 is below x/2^32 < 1/n, so the floor is exact; one v_mul_hi_u32 instead of a division sequence
+__device__ __forceinline__ int fdiv16(int x, uint32_t m) { return m ? (int)__umulhi((uint32_t)x, m) : x; }
 
 __device__ __forceinline__ int region(int p, int P, int w, int s) {
   if (s == 0) return 2;
@@ -54,12 +59,17 @@ __device__ __forceinline__ TokInfo token_info(const dfk_wattn_args& a, const Geo
   return t;
 }
 
-// only the row of token i (the forward's Q/K/V gathers)
+// only the row of token i (the forward's Q/K/V gathers): window origin from uniform values, token
+// offsets by multiply-high divisions, cyclic roll by one conditional subtract (coordinate < 2 * padded dim)
 __device__ __forceinline__ int token_info_row(const dfk_wattn_args& a, const Geo& g, int b, int win, int i) {
   if (i >= g.N) return -2;
   const int wwi = win % g.nww, whi = (win / g.nww) % g.nwh, wdi = win / (g.nww * g.nwh);
-  const int td = i / (a.wh * a.ww), th = (i / a.ww) % a.wh, tw = i % a.ww;
-  const int od = (wdi * a.wd + td + a.sd) % g.Dp, oh = (whi * a.wh + th + a.sh) % g.Hp, ow = (wwi * a.ww + tw + a.sw) % g.Wp;
+  const int td = fdiv16(i, g.m_hw), r = i - td * (a.wh * a.ww);
+  const int th = fdiv16(r, g.m_w), tw = r - th * a.ww;
+  int od = wdi * a.wd + a.sd + td, oh = whi * a.wh + a.sh + th, ow = wwi * a.ww + a.sw + tw;
+  od -= od >= g.Dp ? g.Dp : 0;
+  oh -= oh >= g.Hp ? g.Hp : 0;
+  ow -= ow >= g.Wp ? g.Wp : 0;
   return (od < a.D && oh < a.H && ow < a.W) ? ((b * a.D + od) * a.H + oh) * a.W + ow : -1;
 }
 
@@ -855,6 +865,9 @@ Geo make_geo(const dfk_wattn_args& a) {
   g.L = (2 * a.fd - 1) * (2 * a.fh - 1) * (2 * a.fw - 1);
   g.C0 = ((a.fd - 1) * (2 * a.fh - 1) + (a.fh - 1)) * (2 * a.fw - 1) + (a.fw - 1);
   g.use_mask = (a.sd > 0 || a.sh > 0 || a.sw > 0) ? 1 : 0;
+  auto magic = [](int n) -> uint32_t { return n <= 1 ? 0u : (uint32_t)(0xFFFFFFFFull / (unsigned)n + 1); };
+  g.m_hw = magic(a.wh * a.ww);
+  g.m_w = magic(a.ww);
   return g;
 }
 
@@ -864,6 +877,7 @@ bool args_ok(const dfk_wattn_args& a) {
   if (a.mask && a.mask_nw <= 0) return false;
   if (a.wd <= 0 || a.wh <= 0 || a.ww <= 0 || a.fd <= 0 || a.fh <= 0 || a.fw <= 0) return false;
   if (a.wd * a.wh * a.ww > a.fd * a.fh * a.fw) return false;  // tokens decode inside the full window (Q3)
+  if ((long)a.wd * a.wh * a.ww >= 65536) return false;        // fdiv16 token decode
   if (a.sd < 0 || a.sh < 0 || a.sw < 0 || a.sd >= a.wd || a.sh >= a.wh || a.sw >= a.ww) return false;
   const int vec = a.dtype == DFK_BF16 ? 8 : 4;
   if (a.ld_qkv % vec || a.ld_out % vec) return false;

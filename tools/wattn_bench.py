@@ -38,7 +38,7 @@ def timed(fn):
 
 def main():
     dt = torch.bfloat16
-    for name, dims, win, fw, shift, heads, hd, has_rpb in SHAPES:
+    for name, dims, win, fw, shift, heads, hd, has_rpb in SHAPES + SHAPES[:1]:   # vst1 again, clocks warm
         rows = dims[0] * dims[1] * dims[2] * dims[3]
         C = heads * hd
         qkv = torch.randn(rows, 3 * C, device="cuda").to(dt)
@@ -56,7 +56,7 @@ def main():
         dqkv = torch.empty_like(qkv)
         drpb = torch.zeros_like(rpb) if rpb is not None else None
         tf = timed(lambda: K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, win, fw, shift, heads, hd, scale,
-                                       rpb=rpb, out=out))
+                                       rpb=rpb, out=out, tab=tab))
         tb = timed(lambda: K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, 3 * C, dims, win, fw, shift, heads,
                                         hd, scale, rpb, None), dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C,
                                        drpb=drpb, tab=tab))
