@@ -13,7 +13,15 @@ averages (sum / world, matching the mean BCE loss over the global batch).
 Parameters that never receive a gradient (Audio2D.classifier with
 use_feat=True, Q10) are handled by a final flush: every bucket not yet
 launched is reduced in finish().  Works with the gloo backend for CPU tests.
+
+Gradient accumulation (src/trainer.py:280-297, accum_step micro-batches per
+optimizer step, default 4 at config.py:31): the non-final micro-steps run
+inside ``no_sync()`` — arrivals are ignored, nothing is launched, gradients
+just accumulate in the flat buffer — and only the last micro-step's backward
+launches the bucket all-reduces, each over the sum of every micro-step.
 """
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -45,7 +53,9 @@ class GradBucketer:
         self.works = [None] * len(self.buckets)
         self.enabled = self.world > 1
         self.overlap = True       # hooks launch bucket all-reduces during backward (eager steps)
+        self.sync = True          # False inside no_sync(): accumulation micro-steps launch nothing
         self.hooks = []
+        self.bn_buffers = []
         if self.enabled:
             for i, p in enumerate(store.params):
                 self.hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -57,8 +67,18 @@ class GradBucketer:
             self.pending[b] = len(idx)
             self.works[b] = None
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        """torch DDP.no_sync semantics: backward passes inside only accumulate."""
+        old = self.sync
+        self.sync = False
+        try:
+            yield
+        finally:
+            self.sync = old
+
     def _ready(self, i):
-        if not self.overlap:
+        if not (self.overlap and self.sync):
             return
         b = self.bucket_of[i]
         self.pending[b] -= 1
@@ -73,6 +93,8 @@ class GradBucketer:
         self.works[b] = dist.all_reduce(self.store.grad[s:e], group=self.group, async_op=True)
 
     def finish(self):
+        """After the last micro-step's backward: flush buckets not yet launched (unused
+        parameters), wait for every bucket, average over ranks, re-arm the counters."""
         if not self.enabled:
             return
         for b in range(len(self.buckets)):
@@ -92,8 +114,25 @@ class GradBucketer:
             w.wait()
         self.store.grad.div_(self.world)
 
+    def track_batchnorm(self, module):
+        """Remember the BatchNorm running statistics that broadcast_bn() refreshes every step."""
+        self.bn_buffers = []
+        for m in module.modules():
+            if isinstance(m, torch.nn.modules.batchnorm._BatchNorm) and m.track_running_stats:
+                self.bn_buffers += [m.running_mean, m.running_var]
+        return self
+
+    def broadcast_bn(self, src=0):
+        """Per-step BN running statistics from rank 0 (§8e): the reference's DataParallel
+        re-replicates GPU0's module (buffers included) at every forward, so only GPU0's
+        statistics persist; every rank starts each step from rank 0's."""
+        if not self.enabled:
+            return
+        for buf in self.bn_buffers:
+            dist.broadcast(buf, src, group=self.group)
+
     def broadcast_buffers(self, module, src=0):
-        """BatchNorm running stats from rank 0 (the reference's DP keeps GPU0's, §8e)."""
+        """All floating buffers from rank 0 (identical replicas at start-up)."""
         if not self.enabled:
             return
         for buf in module.buffers():

@@ -21,15 +21,26 @@ class FusedSGD:
         self.lr_dev = torch.full((1,), self.base_lr, device=store.flat.device, dtype=torch.float32)
         self.param_groups = [{"lr": self.base_lr, "initial_lr": self.base_lr}]
         self.first = True
+        self.has_buf = [False] * len(store.params)   # torch: momentum buffer created at a param's first grad
 
     def set_lr(self, lr):
         self.param_groups[0]["lr"] = float(lr)
         self.lr_dev.fill_(float(lr))
 
     def step(self, first=None):
-        f = self.first if first is None else first
-        K.sgd_step(self.store.flat, self.store.grad, self.buf, self.store.shadow, 0.0, self.momentum,
-                   self.weight_decay, f, lr_dev=self.lr_dev)
+        """One SGD step over the parameters that received a gradient (torch skips grad=None:
+        no weight decay and no momentum for them), in as few contiguous launches as possible."""
+        st = self.store
+        if not any(st.touched):          # no bookkeeping (e.g. a captured replay): every parameter
+            runs = [(0, st.numel, self.first if first is None else first)]
+        else:
+            runs = st.touched_runs(also=[not h for h in self.has_buf])
+            for i, t in enumerate(st.touched):
+                if t:
+                    self.has_buf[i] = True
+        for s, e, f in runs:
+            K.sgd_step(st.flat[s:e], st.grad[s:e], self.buf[s:e], st.shadow[s:e] if st.shadow is not None else None,
+                       0.0, self.momentum, self.weight_decay, bool(f), lr_dev=self.lr_dev)
         self.first = False
 
     def zero_grad(self):

@@ -50,19 +50,46 @@ class ParamStore:
         self.index = {id(p): i for i, p in enumerate(self.params)}
         self.uses = {}           # id(p) -> forward uses whose backward has not run yet (direct mode)
         self.listeners = []      # callbacks(i) when parameter i's gradient is complete
+        # parameters that received a gradient since the last zero_grad: torch's SGD skips a
+        # parameter whose .grad is None (no weight decay, no momentum), e.g. Audio2D.classifier
+        # with use_feat=True (Q10) or a LayerDrop-skipped layer; FusedSGD steps only these
+        self.touched = [False] * len(self.params)
+        for i, p in enumerate(self.params):
+            p.register_post_accumulate_grad_hook(self._mark(i))
         self.refresh_shadow()
+
+    def _mark(self, i):
+        def hook(_p):
+            self.touched[i] = True
+        return hook
 
     def grad_ready(self, p):
         """A direct-mode backward finished accumulating into p.grad."""
         k = id(p)
+        i = self.index[k]
+        self.touched[i] = True
         n = self.uses.get(k, 1) - 1
         if n > 0:
             self.uses[k] = n
             return
         self.uses.pop(k, None)
-        i = self.index[k]
         for cb in self.listeners:
             cb(i)
+
+    def touched_runs(self, also=None):
+        """Contiguous [start, end) element ranges of the flat buffers covering the touched
+        parameters (split where ``also[i]`` changes as well)."""
+        runs = []
+        for i, t in enumerate(self.touched):
+            if not t:
+                continue
+            s, e = self.offsets[i], self.offsets[i] + self.params[i].numel()
+            key = also[i] if also is not None else None
+            if runs and runs[-1][2] == key and runs[-1][3] == i - 1:
+                runs[-1] = (runs[-1][0], e, key, i)
+            else:
+                runs.append((s, e, key, i))
+        return [(s, e, k) for s, e, k, _ in runs]
 
     def refresh_shadow(self):
         if self.shadow is not None:
@@ -72,6 +99,7 @@ class ParamStore:
     def zero_grad(self):
         self.grad.zero_()
         self.uses.clear()
+        self.touched = [False] * len(self.params)
 
     def rebind_grads(self):
         """Re-attach .grad views (a user may have set grads to None)."""

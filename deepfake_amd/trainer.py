@@ -37,7 +37,14 @@ def normalize_wave(w):
 
 class TrainStep:
     """fwd + BCE + bwd + gradient all-reduce + SGD for one micro-batch, optionally
-    captured once into a HIP graph and replayed (inputs copied into static buffers)."""
+    captured once into a HIP graph and replayed (inputs copied into static buffers).
+
+    ``micro(feature, label, last, accum)`` is the gradient-accumulation form of
+    src/trainer.py:280-297: loss / accum -> backward for every micro-batch; the
+    non-final ones run under the bucketer's no_sync() (no all-reduce), the final
+    one launches the overlapped bucket all-reduces over the accumulated sum, then
+    SGD and zero_grad.  BatchNorm running statistics are re-broadcast from rank 0
+    at the first micro-step of every optimizer step (§8e)."""
 
     def __init__(self, model, store, opt, bucketer, graph=False):
         self.model, self.store, self.opt, self.bucketer = model, store, opt, bucketer
@@ -45,26 +52,41 @@ class TrainStep:
         self.graph_mode = graph
         self.graph = None
         self.static = None
+        self.first_micro = True
+        if not bucketer.bn_buffers:
+            bucketer.track_batchnorm(model)
 
-    def _fwd_bwd(self, feature, label):
+    def _fwd_bwd(self, feature, label, scale=1.0):
         prob = self.model(feature)
         loss = self.lossF(prob.float().reshape(-1), label.float().reshape(-1))
-        loss.backward()
+        (loss * scale if scale != 1.0 else loss).backward()
         return loss, prob
 
-    def eager(self, feature, label):
-        loss, prob = self._fwd_bwd(feature, label)
+    def micro(self, feature, label, last, accum=1):
+        if self.first_micro:
+            self.bucketer.broadcast_bn()
+            self.first_micro = False
+        if not last:
+            with self.bucketer.no_sync():
+                loss, prob = self._fwd_bwd(feature, label, 1.0 / accum)
+            return loss.detach(), prob.detach()
+        loss, prob = self._fwd_bwd(feature, label, 1.0 / accum)
         self.bucketer.finish()          # overlapped bucket all-reduces (hooks), then average
         self.opt.step()                 # first call initialises the momentum buffer (torch SGD semantics)
         self.store.zero_grad()
+        self.first_micro = True
         # detach: a live autograd graph would pin AccumulateGrad nodes to this stream (breaks capture)
         return loss.detach(), prob.detach()
+
+    def eager(self, feature, label):
+        return self.micro(feature, label, True, 1)
 
     def __call__(self, feature, label):
         if not self.graph_mode:
             return self.eager(feature, label)
         if self.graph is None:
             return self._capture(feature, label)
+        self.bucketer.broadcast_bn()
         for s, x in zip(self.static[0], feature):
             s.copy_(x, non_blocking=True)
         self.static[1].copy_(label, non_blocking=True)
@@ -197,13 +219,7 @@ class Trainer:
                 if self.accum_step == 1:
                     loss, prob = self.step_fn(feature, label)
                 else:
-                    r = self.run_batch(feature, label)
-                    (r["loss"] / self.accum_step).backward()
-                    loss = r["loss"]
-                    if last:
-                        self.bucketer.finish()
-                        self.optimizer.step()
-                        self.store.zero_grad()
+                    loss, prob = self.step_fn.micro(feature, label, last, self.accum_step)
                 if last:
                     t += 1
                     self.scheduler.step()

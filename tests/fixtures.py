@@ -25,6 +25,20 @@ def rel_err(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-12))
 
 
+def error(fx, key, t):
+    """max|a-b| / max|b| of tensor t against fixture key (full array, or the @sub sample and the
+    @norm of a compressed one, whichever is worse); raises on a shape mismatch only."""
+    a = t.detach().float().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+    if key in fx:
+        assert a.shape == fx[key].shape, f"{key}: shape {a.shape} vs {fx[key].shape}"
+        return rel_err(a, fx[key])
+    step = int(fx[key + "@step"])
+    assert tuple(a.shape) == tuple(fx[key + "@shape"]), f"{key}: shape"
+    e = rel_err(a.reshape(-1)[::step], fx[key + "@sub"])
+    nrm = float(np.sqrt((a.astype(np.float64) ** 2).sum()))
+    return max(e, abs(nrm - float(fx[key + "@norm"])) / max(float(fx[key + "@norm"]), 1e-12))
+
+
 def check(fx, key, t, rtol, what=""):
     """Compare tensor t to fixture key (full array, or @sub/@sum/@norm summary).
     Error is max|a-b| / max|b| (relative to the tensor's scale)."""

@@ -63,14 +63,37 @@ FUSED_C1 = dict(
     w2v_layers=2, video_dim=768, audio_dim=256)
 
 
-def fixture_compress(key, a, big=65536):
+# ---------------------------------------------------------------- C2 shapes
+# Swin-T stage-1 SW-MSA block over a whole C2 clip's stage-1 volume: N=392 windows, shift (4,3,3)
+BLOCK_C2_S1 = dict(name="block_c2_s1", dim=96, heads=3, window=(8, 7, 7), shift=(4, 3, 3), shape=(1, 16, 56, 56),
+                   seed=151)
+# stage 4: H=W=7 <= window -> get_window_size keeps only the D shift (4,0,0) (Q6); 2 windows along D
+BLOCK_C2_S4 = dict(name="block_c2_s4", dim=768, heads=24, window=(8, 7, 7), shift=(4, 3, 3), shape=(1, 16, 7, 7),
+                   seed=161)
+# SwinV2-B mel stage 3 (C2 mel branch): 14x14 tokens, C=512, 16 heads, window 7, blocks shift 0 / 3,
+# pretrained_window_size 16 (the CPB-MLP coordinate normalisation), two clips
+MEL_C2_S3 = dict(name="mel_c2_s3", dim=512, heads=16, res=(14, 14), window=7, pretrained=16, B=2, seed=171)
+
+FUSED_C2 = dict(
+    name="fused_c2", seed=181, B=2, T=32, H=224, W=224, seconds=4, lr=0.01, wd=0.05,
+    vst=dict(patch_size=(2, 4, 4), embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24],
+             window_size=(8, 7, 7), drop_path_rate=0.0, patch_norm=True),
+    mel=dict(num_classes=1, use_feat=True, embed_dim=128, depths=[2, 2, 18, 2], num_heads=[4, 8, 16, 32],
+             window_size=7, drop_path_rate=0.0, pretrained_window_sizes=(16, 16, 16, 16)),
+    w2v_layers=12, video_dim=768, audio_dim=1024)
+
+GRAD_SAMPLE_C1 = 1024   # per-parameter gradient tensors of the fused train steps: strided samples + norm
+GRAD_SAMPLE_C2 = 512
+
+
+def fixture_compress(key, a, big=65536, sample=8192):
     """Tensors above ``big`` elements are stored as key@sub (every step-th
-    element of the flat array), key@sum and key@norm (float64)."""
+    element of the flat array, about ``sample`` of them), key@sum and key@norm (float64)."""
     import numpy as np
     a = np.asarray(a)
     if a.size <= big:
         return {key: a}
-    step = -(-a.size // 8192)
+    step = -(-a.size // sample)
     f = a.reshape(-1).astype(np.float64)
     return {key + "@sub": a.reshape(-1)[::step].copy(), key + "@step": np.array(step),
             key + "@shape": np.array(a.shape), key + "@sum": np.array(f.sum()),

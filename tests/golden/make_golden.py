@@ -34,11 +34,11 @@ VST = R.VST
 BIG = 65536  # larger tensors are stored as a strided sample + sum + norm (fixture_compress)
 
 
-def save(name, **arrays):
+def save(name, _big=BIG, _sample=8192, **arrays):
     out = {}
     for k, v in arrays.items():
         a = v.detach().cpu().numpy() if hasattr(v, "detach") else np.asarray(v)
-        out.update(GC.fixture_compress(k, a, BIG))
+        out.update(GC.fixture_compress(k, a, _big, _sample))
     path = os.path.join(HERE, f"{name}.npz")
     np.savez_compressed(path, **out)
     print(f"{name}: " + ", ".join(f"{k}{tuple(v.shape)}" for k, v in out.items()))
@@ -64,22 +64,47 @@ def case_window_attention():
         save(c["name"], y=y, dx=x.grad, **grads_of(m))
 
 
+def _block(c):
+    m = VST.SwinTransformerBlock3D(c["dim"], c["heads"], window_size=tuple(c["window"]),
+                                   shift_size=tuple(c["shift"]), qkv_bias=True)
+    named_fill_(m, seed=c["seed"])
+    B, D, H, W = c["shape"]
+    x = randn(c["seed"] + 1, (B, D, H, W, c["dim"])).requires_grad_(True)
+    ws, ss = VST.get_window_size((D, H, W), tuple(c["window"]), tuple(c["shift"]))
+    Dp = -(-D // ws[0]) * ws[0]
+    Hp = -(-H // ws[1]) * ws[1]
+    Wp = -(-W // ws[2]) * ws[2]
+    mask = VST.compute_mask(Dp, Hp, Wp, ws, ss, torch.device("cpu"))
+    y = m(x, mask)
+    gy = randn(c["seed"] + 2, y.shape)
+    y.backward(gy)
+    save(c["name"], y=y, dx=x.grad, **grads_of(m))
+
+
 def case_block():
     for c in GC.BLOCK_CASES:
-        m = VST.SwinTransformerBlock3D(c["dim"], c["heads"], window_size=tuple(c["window"]),
-                                       shift_size=tuple(c["shift"]), qkv_bias=True)
-        named_fill_(m, seed=c["seed"])
-        B, D, H, W = c["shape"]
-        x = randn(c["seed"] + 1, (B, D, H, W, c["dim"])).requires_grad_(True)
-        ws, ss = VST.get_window_size((D, H, W), tuple(c["window"]), tuple(c["shift"]))
-        Dp = -(-D // ws[0]) * ws[0]
-        Hp = -(-H // ws[1]) * ws[1]
-        Wp = -(-W // ws[2]) * ws[2]
-        mask = VST.compute_mask(Dp, Hp, Wp, ws, ss, torch.device("cpu"))
-        y = m(x, mask)
-        gy = randn(c["seed"] + 2, y.shape)
-        y.backward(gy)
-        save(c["name"], y=y, dx=x.grad, **grads_of(m))
+        _block(c)
+
+
+def case_block_c2():
+    """C2 geometry: the stage-1 SW-MSA launch the bench's roofline reports (N=392, shift 4x3x3,
+    a whole clip's 16x56x56 volume) and the stage-4 D-only shift (4,0,0) at 16x7x7."""
+    _block(GC.BLOCK_C2_S1)
+    _block(GC.BLOCK_C2_S4)
+
+
+def case_mel_c2():
+    """SwinV2-B mel stage-3 block pair (reference BasicLayer: W-MSA then SW-MSA shift 3)."""
+    c = GC.MEL_C2_S3
+    m = R.S2.BasicLayer(dim=c["dim"], input_resolution=c["res"], depth=2, num_heads=c["heads"],
+                        window_size=c["window"], pretrained_window_size=c["pretrained"])
+    named_fill_(m, seed=c["seed"])
+    H, W = c["res"]
+    x = randn(c["seed"] + 1, (c["B"], H * W, c["dim"])).requires_grad_(True)
+    y = m(x)
+    gy = randn(c["seed"] + 2, y.shape)
+    y.backward(gy)
+    save(c["name"], y=y, dx=x.grad, **grads_of(m))
 
 
 def case_patch_embed_merge():
@@ -213,9 +238,80 @@ def case_fused_c1():
     save(c["name"], p_eval=pe, z_eval=z_eval, p_train=p, z_train=logits["z"], loss=loss, **gnorm, **psum)
 
 
+def _sampled_err(a, ref, sample):
+    """The parity tests' error metric (tests/fixtures.error) on the fixture's own sampling."""
+    a, ref = a.double().reshape(-1), ref.double().reshape(-1)
+    step = -(-ref.numel() // sample) if ref.numel() > sample else 1
+    e = ((a[::step] - ref[::step]).abs().max() / ref[::step].abs().max().clamp_min(1e-12)).item()
+    en = abs(a.norm().item() - ref.norm().item()) / max(ref.norm().item(), 1e-12)
+    return max(e, en)
+
+
+def _fused_train_grads(c, sample):
+    """One training forward + BCE backward of the reference fused model (src/trainer.py:124-148,280-282);
+    returns the per-parameter gradient tensors (compressed) and the step's outputs.
+
+    The same step is also run under the reference's own bf16 autocast (torch.autocast(bfloat16) on CPU):
+    ``ea:<param>`` is that run's gradient error against the fp32 one, in the parity tests' metric — the
+    error bf16 arithmetic itself costs this model, which bounds what any bf16 implementation can meet."""
+    m = build_fused_ref(c)
+    named_fill_(m, seed=c["seed"])
+    video, mel, wave, label = synthetic_inputs(c["B"], c["T"], c["H"], c["W"], c["seconds"], seed=c["seed"] + 1)
+    logits = {}
+    m.classify.register_forward_hook(lambda mod, i, o: logits.__setitem__("z", o.detach().clone()))
+    m.eval()
+    with torch.no_grad():
+        pe = m((video, mel, wave))
+    z_eval = logits["z"]
+    m.train()
+    p = m((video, mel, wave))
+    loss = torch.nn.BCELoss()(p, label)
+    loss.backward()
+    z_train = logits["z"]
+    g = {("g:" + n): q.grad.clone() for n, q in m.named_parameters() if q.grad is not None}
+    m2 = build_fused_ref(c)
+    named_fill_(m2, seed=c["seed"])
+    m2.train()
+    m2.classify.register_forward_hook(lambda mod, i, o: logits.__setitem__("z", o.detach().clone()))
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        p2 = m2((video, mel, wave))
+    torch.nn.BCELoss()(p2.float(), label).backward()
+    ea = {("ea:" + n): _sampled_err(q.grad, g["g:" + n], sample)
+          for n, q in m2.named_parameters() if q.grad is not None and ("g:" + n) in g}
+    za = (logits["z"].double() - z_train.double()).abs().max() / z_train.double().abs().max()
+    return m, dict(p_eval=pe, z_eval=z_eval, p_train=p, z_train=z_train, loss=loss, ea_logits=za, **g, **ea)
+
+
+def case_fused_c1_grads():
+    """The fused C1 train step's per-parameter gradient TENSORS (strided samples + norms)."""
+    c = GC.FUSED_C1
+    _, out = _fused_train_grads(c, GC.GRAD_SAMPLE_C1)
+    save("fused_c1_grads", _big=GC.GRAD_SAMPLE_C1, _sample=GC.GRAD_SAMPLE_C1, **out)
+
+
+def case_fused_c2():
+    """The whole north-star model at C2 shapes (Swin-T 32x224x224, SwinV2-B mel, wav2vec2-base 4 s), B=2:
+    eval logits/probabilities and one training forward+backward with every gradient tensor (sampled)."""
+    c = GC.FUSED_C2
+    _, out = _fused_train_grads(c, GC.GRAD_SAMPLE_C2)
+    save(c["name"], _big=GC.GRAD_SAMPLE_C2, _sample=GC.GRAD_SAMPLE_C2, **out)
+
+
+def case_state_keys():
+    """state_dict keys + shapes of the reference fused model at C1 and C2 (371 keys at C1)."""
+    import json
+    out = {}
+    for c in (GC.FUSED_C1, GC.FUSED_C2):
+        sd = build_fused_ref(c).state_dict()
+        out[c["name"]] = [[k, list(v.shape)] for k, v in sd.items()]
+    with open(os.path.join(HERE, "state_keys.json"), "w") as f:
+        json.dump(out, f)
+    print("state_keys:", {k: len(v) for k, v in out.items()})
+
+
 if __name__ == "__main__":
     only = sys.argv[1:]
     for fn in [case_window_attention, case_block, case_patch_embed_merge, case_vst_c1, case_w2v, case_head,
-               case_fused_c1]:
+               case_fused_c1, case_block_c2, case_mel_c2, case_fused_c1_grads, case_fused_c2, case_state_keys]:
         if not only or fn.__name__ in only:
             fn()

@@ -72,5 +72,6 @@ def import_reference():
     from src.models.ModalFusion import FusionModel
     from src.models.audioTransformer import Audio2D
     from src.models.swin_transformer2d import SwinTransformerV2
+    S2 = sys.modules["src.models.swin_transformer2d"]
     return types.SimpleNamespace(U=U, VST=VST, FusionModel=FusionModel, Audio2D=Audio2D,
-                                 SwinTransformerV2=SwinTransformerV2, torch=torch)
+                                 SwinTransformerV2=SwinTransformerV2, S2=S2, torch=torch)

@@ -79,6 +79,82 @@ def _worker(rank, world, port, overlap, q):
     dist.destroy_process_group()
 
 
+class ProbNet(Net):
+    def forward(self, x):
+        return torch.sigmoid(super().forward(x[0]))
+
+
+class _PlainSGD:
+    """CPU stand-in for FusedSGD (the HIP kernel): flat -= lr * grad."""
+
+    def __init__(self, store, lr):
+        self.store, self.lr = store, lr
+
+    def step(self):
+        self.store.flat.add_(self.store.grad, alpha=-self.lr)
+
+
+def _label(seed, n):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(n, generator=g) < 0.5).float()
+
+
+ACC, MB = 2, 2   # micro-steps per optimizer step, clips per micro-batch per rank
+
+
+def _accum_worker(rank, world, port, q):
+    from deepfake_amd.trainer import TrainStep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m = ProbNet()
+    m.train()
+    store = ParamStore(m, torch.float32, device=torch.device("cpu"))
+    bk = GradBucketer(store, bucket_mb=0.0002)
+    step = TrainStep(m, store, _PlainSGD(store, 0.1), bk)
+    x, _ = _data(2, world * ACC * MB)
+    lab = _label(3, world * ACC * MB)
+    launched_early = []
+    if rank == 0:
+        m.bn.running_mean.fill_(5.0)      # rank 0's statistics win at the next step's broadcast
+    for k in range(ACC):
+        i0 = (rank * ACC + k) * MB
+        step.micro((x[i0:i0 + MB],), lab[i0:i0 + MB], last=(k == ACC - 1), accum=ACC)
+        if k < ACC - 1:
+            launched_early.append(any(w is not None for w in bk.works))
+    step.bucketer.broadcast_bn()
+    q.put((rank, store.flat.clone(), m.bn.running_mean.clone(), launched_early))
+    dist.destroy_process_group()
+
+
+def test_accumulation_no_sync_matches_single_process_sum():
+    """world 2 x accum_step 2 == one process summing the 4 micro-batches (each loss / 4), then one SGD
+    step; non-final micro-steps launch no all-reduce (no_sync); BN statistics follow rank 0."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_accum_worker, args=(r, 2, 29513, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (f, rm, le)) for r, f, rm, le in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+    torch.manual_seed(0)
+    m = ProbNet()
+    m.train()
+    store = ParamStore(m, torch.float32, device=torch.device("cpu"))
+    x, _ = _data(2, 2 * ACC * MB)
+    lab = _label(3, 2 * ACC * MB)
+    for j in range(2 * ACC):
+        p = m((x[j * MB:(j + 1) * MB],))
+        (torch.nn.BCELoss()(p, lab[j * MB:(j + 1) * MB]) / (2 * ACC)).backward()
+    store.flat.add_(store.grad, alpha=-0.1)
+    for r in range(2):
+        f, rm, le = res[r]
+        assert not any(le), "an all-reduce was launched inside no_sync"
+        assert torch.allclose(f, store.flat, atol=1e-6), (r, (f - store.flat).abs().max())
+    assert torch.equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("overlap", [True, False])
 def test_bucketed_allreduce_matches_global_batch(overlap):
     ctx = mp.get_context("spawn")
