@@ -6,7 +6,9 @@ Workload (BASELINE.json configs[1], "C2"): Video Swin-T (depths 2,2,6,2, window
 over a 224x224 mel image + wav2vec2-base over 4 s @ 16 kHz + FusionModel head;
 B=8 clips per GPU; bf16 compute (fp32 master weights, fp32 softmax/LN stats);
 one step = forward + BCE + backward + RCCL gradient all-reduce + fused SGD
-(momentum 0.9, wd) — the whole step captured in one HIP graph and replayed.
+(momentum 0.9, wd) — the whole step captured in one HIP graph and replayed
+(the first warm-up step runs eagerly and captures; --eager replays nothing), with
+the video / mel / waveform trunks on three HIP streams inside the graph.
 Inputs are synthetic, generated on device and resident in HBM.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -41,7 +43,7 @@ def parse():
     p.add_argument("--config", default="c2")
     p.add_argument("--batch", type=int, default=8)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    p.add_argument("--graph", action="store_true", help="capture the whole step in one HIP graph (experimental)")
+    p.add_argument("--eager", action="store_true", help="run the step eagerly instead of replaying its HIP graph")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--roofline-iters", type=int, default=20)
@@ -205,7 +207,7 @@ def main():
         dist.broadcast(store.flat, 0)
         store.refresh_shadow()
     opt = FusedSGD(store, lr=1e-4, momentum=0.9, weight_decay=1e-3)
-    step = TrainStep(model, store, opt, bucketer, graph=a.graph)
+    step = TrainStep(model, store, opt, bucketer, graph=not a.eager)
     feature, label = synthetic_batch(cfg, a.batch, device, 1234 + rank)
 
     for _ in range(max(a.warmup, 1)):
@@ -247,7 +249,7 @@ def main():
             "config": {"workload": f"{a.config.upper()}: Swin-T video 32x224x224 (window 8x7x7) + SwinV2 mel 224 + "
                                    f"wav2vec2-base 4s@16kHz + FusionModel, full train step",
                        "global_batch": world * a.batch, "per_gpu_batch": a.batch,
-                       "parallelism": f"dp{world}", "hip_graph": a.graph, "loss": round(lossv, 5)},
+                       "parallelism": f"dp{world}", "hip_graph": not a.eager, "branch_streams": 3, "loss": round(lossv, 5)},
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2) if train_gflop else None,
             "roofline": roof, "roofline_conv3d": roof_conv, "cpu_baseline": cpu,
         }

@@ -56,6 +56,8 @@ class GradBucketer:
         self.sync = True          # False inside no_sync(): accumulation micro-steps launch nothing
         self.hooks = []
         self.bn_buffers = []
+        self.streams = []         # branch streams whose kernels write gradients (FusionModel.branch_streams)
+        self.comm_stream = None
         if self.enabled:
             for i, p in enumerate(store.params):
                 self.hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -90,7 +92,19 @@ class GradBucketer:
 
     def _launch(self, b):
         s, e, _ = self.buckets[b]
-        self.works[b] = dist.all_reduce(self.store.grad[s:e], group=self.group, async_op=True)
+        if not self.streams or not self.store.grad.is_cuda:
+            self.works[b] = dist.all_reduce(self.store.grad[s:e], group=self.group, async_op=True)
+            return
+        # a bucket may hold gradients written on several branch streams: issue the all-reduce from a
+        # comm stream that waits for all of them (RCCL orders itself after the issuing stream)
+        if self.comm_stream is None:
+            self.comm_stream = torch.cuda.Stream()
+        cs = self.comm_stream
+        cs.wait_stream(torch.cuda.current_stream())
+        for st in self.streams:
+            cs.wait_stream(st)
+        with torch.cuda.stream(cs):
+            self.works[b] = dist.all_reduce(self.store.grad[s:e], group=self.group, async_op=True)
 
     def finish(self):
         """After the last micro-step's backward: flush buckets not yet launched (unused

@@ -57,9 +57,43 @@ class FusionModel(nn.Module):
         self.last_logits = z.detach()
         return self.out_act(z.squeeze())
 
+    parallel_branches = False    # set by the training runtime (TrainStep), which also joins the streams
+
+    def branch_streams(self):
+        if not hasattr(self, "_streams"):
+            self._streams = [torch.cuda.Stream() for _ in range(3)]
+        return self._streams
+
+    def join_branches(self):
+        """Make the current stream wait for every branch stream (after backward: the direct-mode
+        weight gradients the branch kernels wrote into the flat buffer)."""
+        if hasattr(self, "_streams"):
+            cur = torch.cuda.current_stream()
+            for s in self._streams:
+                cur.wait_stream(s)
+
     def forward(self, feature: tuple):
+        """ModalFusion.py:30-75.  The three extractors are independent until the head: with
+        parallel_branches they run on three HIP streams (video / mel / waveform), so the small-M
+        GEMMs of the mel and wav2vec2 trunks fill the CUs the HBM-bound video trunk leaves idle; the
+        autograd engine runs each backward op on its forward op's stream, so backward overlaps too."""
         video_feat, audio_feat, paudio_feat = feature
-        return self.head(self.vExtract(video_feat), self.aExtract(audio_feat), self.paExtract(paudio_feat))
+        if not (self.parallel_branches and video_feat.is_cuda):
+            return self.head(self.vExtract(video_feat), self.aExtract(audio_feat), self.paExtract(paudio_feat))
+        cur = torch.cuda.current_stream()
+        capturing = torch.cuda.is_current_stream_capturing()
+        outs = []
+        for s, ext, x in zip(self.branch_streams(), (self.vExtract, self.aExtract, self.paExtract), feature):
+            s.wait_stream(cur)
+            if not capturing:
+                x.record_stream(s)
+            with torch.cuda.stream(s):
+                outs.append(ext(x))
+        for s, o in zip(self._streams, outs):
+            cur.wait_stream(s)
+            if not capturing:
+                o.record_stream(cur)
+        return self.head(*outs)
 
     def cal_nce_loss(self, p_a, p_b):
         """ModalFusion.py:78-99 (unused by the reference's training; kept for the API)."""

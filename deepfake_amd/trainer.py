@@ -46,8 +46,12 @@ class TrainStep:
     SGD and zero_grad.  BatchNorm running statistics are re-broadcast from rank 0
     at the first micro-step of every optimizer step (§8e)."""
 
-    def __init__(self, model, store, opt, bucketer, graph=False):
+    def __init__(self, model, store, opt, bucketer, graph=False, parallel_branches=True):
         self.model, self.store, self.opt, self.bucketer = model, store, opt, bucketer
+        if parallel_branches and hasattr(model, "parallel_branches") and torch.cuda.is_available() \
+                and store.flat.is_cuda:
+            model.parallel_branches = True
+            bucketer.streams = model.branch_streams()
         self.lossF = torch.nn.BCELoss()
         self.graph_mode = graph
         self.graph = None
@@ -60,6 +64,8 @@ class TrainStep:
         prob = self.model(feature)
         loss = self.lossF(prob.float().reshape(-1), label.float().reshape(-1))
         (loss * scale if scale != 1.0 else loss).backward()
+        if getattr(self.model, "parallel_branches", False):
+            self.model.join_branches()
         return loss, prob
 
     def micro(self, feature, label, last, accum=1):
@@ -104,12 +110,21 @@ class TrainStep:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         self.bucketer.overlap = False
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                self.store.grad.zero_()
-                l2, p2 = self._fwd_bwd(tuple(static_in), static_label)
-                self.bucketer.allreduce_all()
-                self.opt.step(first=False)
+        try:
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    self.store.grad.zero_()
+                    l2, p2 = self._fwd_bwd(tuple(static_in), static_label)
+                    self.bucketer.allreduce_all()
+                    self.opt.step(first=False)
+        except RuntimeError as e:         # e.g. a collective the backend cannot capture: stay eager
+            torch.cuda.synchronize()
+            self.bucketer.overlap = True
+            self.bucketer.reset()
+            self.graph_mode = False
+            print(f"[deepfake_amd] HIP-graph capture failed ({e}); running the step eagerly", flush=True)
+            self.store.zero_grad()
+            return loss, prob
         torch.cuda.current_stream().wait_stream(s)
         self.bucketer.overlap = True
         self.bucketer.reset()

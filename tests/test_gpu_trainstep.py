@@ -1,0 +1,56 @@
+"""The training runtime's step (deepfake_amd.trainer.TrainStep: flat ParamStore in direct-gradient mode,
+fused SGD, the three extractors on parallel HIP streams, optional whole-step HIP-graph capture) gives
+the same parameters as the plain sequential eager step, at C1 shapes in fp32 parity mode.
+(src/trainer.py:280-297: forward, BCE, backward, SGD(momentum 0.9, weight decay), zero_grad.)"""
+import pytest
+import torch
+
+import golden_cases as GC
+from oracle.fill import named_fill_, synthetic_inputs
+
+pytestmark = pytest.mark.gpu
+if torch.cuda.is_available():
+    from deepfake_amd.ddp import GradBucketer
+    from deepfake_amd.models.fused import build_fused
+    from deepfake_amd.optim import FusedSGD
+    from deepfake_amd.params import ParamStore
+    from deepfake_amd.trainer import TrainStep
+
+DEV = "cuda"
+
+
+def _run(steps, parallel, graph, dt=torch.float32):
+    c = GC.FUSED_C1
+    m = named_fill_(build_fused("c1", compute_dtype=dt), c["seed"]).to(DEV)
+    m.train()
+    store = ParamStore(m, dt)
+    step = TrainStep(m, store, FusedSGD(store, 0.01, 0.9, 0.05), GradBucketer(store), graph=graph,
+                     parallel_branches=parallel)
+    losses = []
+    for i in range(steps):
+        v, mel, w, lab = synthetic_inputs(c["B"], c["T"], c["H"], c["W"], c["seconds"], seed=c["seed"] + 10 * i)
+        loss, _ = step((v.to(DEV), mel.to(DEV), w.to(DEV)), lab.to(DEV))
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    return store.flat.clone(), losses, m
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / b.abs().max())
+
+
+def test_parallel_branches_match_sequential():
+    ref, lref, m0 = _run(2, parallel=False, graph=False)
+    got, lgot, m1 = _run(2, parallel=True, graph=False)
+    assert not m0.parallel_branches and m1.parallel_branches
+    assert max(abs(a - b) for a, b in zip(lgot, lref)) < 1e-5, (lgot, lref)
+    assert _rel(got, ref) < 1e-5
+
+
+def test_graph_captured_step_matches_eager():
+    """Step 1 runs eager and captures the step; steps 2-3 replay the graph on new inputs copied into the
+    captured buffers; parameters and losses equal three eager steps."""
+    ref, lref, _ = _run(3, parallel=True, graph=False)
+    got, lgot, _ = _run(3, parallel=True, graph=True)
+    assert max(abs(a - b) for a, b in zip(lgot, lref)) < 1e-5, (lgot, lref)
+    assert _rel(got, ref) < 1e-5
