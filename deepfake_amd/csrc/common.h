@@ -76,3 +76,6 @@ __device__ __forceinline__ float wave_max(float v) {
   do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
 
 static inline int dfk_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// weight-resident streaming GEMM (wres.hip): 1 = launched, 0 = not applicable, < 0 = launch error
+int dfk_wres_try(const dfk_gemm_args& g, hipStream_t s);

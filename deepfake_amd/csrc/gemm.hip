@@ -494,6 +494,10 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   if (g.act && g.act != 1 && !g.aux) return DFK_EINVAL;
   if (g.rowsum && (g.nz0 != 1 || g.nz1 != 1 || !g.a_kmajor || !g.b_kmajor)) return DFK_EINVAL;
   if (g.M <= 0 || g.N <= 0) return 0;
+  if constexpr (sizeof(T) == 2) {
+    const int w = dfk_wres_try(g, s);     // huge-M / small-weight Linears: weight-resident streaming kernel
+    if (w != 0) return w > 0 ? 0 : w;
+  }
   // split-K through fp32 slabs + a reduce/epilogue kernel: caller-chosen (splitk > 1, no atomics) or
   // automatic for grids too small to fill the chip
   const int autos = g.splitk > 1 && !g.atomic ? g.splitk : (g.ws ? auto_splitk<T>(g) : 1);

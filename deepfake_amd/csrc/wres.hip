@@ -1,0 +1,254 @@
+// Weight-resident streaming GEMM for the HBM-bound Linears of the Swin stages 1-2 (and the mel
+// branch's stage 1): C[M, N] = A[M, K] . W^T with a small weight (N*K <= WRES_LIMIT elements per
+// column slice) and a huge token count M (50k-400k rows).  dfk_gemm routes such launches here.
+//
+// Why a separate kernel: with K = 96..384 the tiled GEMM's k-loop is 2-6 steps long, so every
+// output tile pays a full prologue (two dependent global->LDS->MFMA round trips) and only one tile
+// per workgroup is ever in flight: the stage-1 qkv Linear (401k x 96 -> 288) ran at 1.5 TB/s of the
+// 8 TB/s HBM roofline.  Here a persistent workgroup loads its W column slice into LDS ONCE and then
+// streams 128-row tiles of A: each wave owns 16 rows, loads its A fragments straight from HBM into
+// registers (16-B loads in MFMA fragment order, no LDS round trip), prefetches the next tile's
+// fragments while it computes the current one, and stores its outputs without LDS staging.
+//
+// Operand order is swapped (D = W . A^T) so that every lane ends up with FOUR CONSECUTIVE OUTPUT
+// CHANNELS of one token: v_mfma_f32_16x16x32_bf16 leaves D[n = 4*(l>>4) + r][m = l&15] in lane l,
+// so bias / residual / aux / C are 8-byte vector accesses along a token row.
+//
+//   W operand: B view rows = output channels j; b_kmajor = 0: W[j][k] (nn.Linear weight, forward),
+//              b_kmajor = 1: W[k][j] (the dX GEMM dy . W reads the weight transposed)
+//   A operand: a_kmajor = 0 only (token rows, k contiguous), bf16.
+#include <algorithm>
+
+#include "common.h"
+
+namespace {
+
+constexpr int WRES_LIMIT = 49152;      // W slice elements (96 KiB bf16) -> one 8-wave workgroup per CU
+constexpr int NT = 512;                // 8 waves x 16 token rows = 128-row tiles
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int KC, int NBW, int NSPLIT>
+constexpr int wres_lds() { return (NBW * 16 * NSPLIT * (KC * 32 + 8) + 8 * 16 * (NBW * 16 + 8)) * 2; }
+
+// two workgroups per CU (4 waves per SIMD, <= 128 VGPRs) only for the smallest wave tile: every other
+// variant spills at 128 VGPRs
+template <int KC, int NBW, int NSPLIT>
+constexpr bool wres_two_per_cu() { return KC == 3 && NBW == 6 && NSPLIT == 1 && wres_lds<KC, NBW, NSPLIT>() <= 80 * 1024; }
+
+template <int KC, int NBW, int NSPLIT>
+__global__ __launch_bounds__(512, (wres_two_per_cu<KC, NBW, NSPLIT>() ? 4 : 2))
+void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
+  // slice of BN = NSPLIT*NBW*16 output channels; the 8 waves form (8/NSPLIT) row groups x NSPLIT column
+  // groups, each wave computing 16 tokens x NBW*16 channels (few accumulators -> several waves per SIMD)
+  constexpr int K = KC * 32, BN = NBW * 16 * NSPLIT, WS = K + 8;   // LDS row stride (elements), padded 16 B
+  constexpr int ROWS_T = 16 * (8 / NSPLIT);
+  constexpr int SS = NBW * 16 + 8;                                 // output staging row stride
+  __shared__ __attribute__((aligned(16))) bf16raw w_lds[BN * WS + 8 * 16 * SS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  bf16raw* stg = w_lds + BN * WS + wave * 16 * SS;
+  const bool staged = g.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0 && g.N % 8 == 0 &&
+                      (!g.aux || (g.ldaux % 8 == 0 && (reinterpret_cast<uintptr_t>(g.aux) & 15) == 0));
+  const int rg = wave / NSPLIT, cg = wave % NSPLIT;
+  const int slice = blockIdx.x % nslices;
+  const int n0 = slice * BN;
+  const int stride = gridDim.x / nslices;
+  const bf16raw* W = reinterpret_cast<const bf16raw*>(g.b.ptr);
+
+  // ---- W slice -> LDS [BN][K] (rows past N zero-filled)
+  if (!g.b_kmajor) {            // W[j][k]: rows of K contiguous elements, 16-B copies
+    for (int idx = tid; idx < BN * (K / 8); idx += NT) {
+      const int j = idx / (K / 8), kc = (idx % (K / 8)) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n0 + j < g.N) v = *reinterpret_cast<const uint4*>(W + (long)(n0 + j) * g.b.ld + kc);
+      *reinterpret_cast<uint4*>(w_lds + j * WS + kc) = v;
+    }
+  } else {                      // W[k][j]: 8 output channels of one k per 16-B load, transposed into LDS
+    for (int idx = tid; idx < K * (BN / 8); idx += NT) {
+      const int k = idx / (BN / 8), jc = (idx % (BN / 8)) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n0 + jc < g.N) v = *reinterpret_cast<const uint4*>(W + (long)k * g.b.ld + n0 + jc);
+      const bf16raw* e = reinterpret_cast<const bf16raw*>(&v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w_lds[(jc + i) * WS + k] = e[i];
+    }
+  }
+  __syncthreads();
+
+  const bf16raw* A = reinterpret_cast<const bf16raw*>(g.a.ptr);
+  const bf16raw* bias = reinterpret_cast<const bf16raw*>(g.bias);
+  const bf16raw* res = reinterpret_cast<const bf16raw*>(g.residual);
+  bf16raw* aux = reinterpret_cast<bf16raw*>(g.aux);
+  bf16raw* C = reinterpret_cast<bf16raw*>(g.c);
+  const int mrow = lane & 15, kq = (lane >> 4) * 8, nq = (lane >> 4) * 4;
+  const bf16raw* wbase = w_lds + (cg * NBW * 16 + mrow) * WS + kq;
+
+  // this wave's fragment row of tile t: token m = t*ROWS_T + rg*16 + (lane&15)
+  auto load_a = [&](int t, uint4 (&fr)[KC]) {
+    const long m = (long)t * ROWS_T + rg * 16 + mrow;
+    const bool ok = m < g.M;
+    const bf16raw* p = A + (ok ? m : 0) * g.a.ld + kq;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      uint4 v = *reinterpret_cast<const uint4*>(p + kc * 32);
+      if (!ok) v = make_uint4(0, 0, 0, 0);
+      fr[kc] = v;
+    }
+  };
+
+  auto process = [&](int t, const uint4 (&a_cur)[KC]) {
+    const long m = (long)t * ROWS_T + rg * 16 + mrow;
+    const bool mok = m < g.M;
+
+    f32x4 acc[NBW];
+#pragma unroll
+    for (int nb = 0; nb < NBW; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // W fragments stream from LDS through a 4-deep register ring (each is used by exactly one MFMA):
+    // the read for step i+RING-1 is issued before MFMA i, and a scheduling barrier keeps the compiler
+    // from hoisting all KC*NBW reads to the top (that spilled the accumulators)
+    constexpr int T = KC * NBW, RING = 4;
+    auto wfrag = [&](int i) {
+      return *reinterpret_cast<const bf16x8*>(wbase + (i % NBW) * 16 * WS + (i / NBW) * 32);
+    };
+    bf16x8 wr[RING];
+#pragma unroll
+    for (int i = 0; i < RING - 1 && i < T; ++i) wr[i] = wfrag(i);
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+      if (i + RING - 1 < T) wr[(i + RING - 1) % RING] = wfrag(i + RING - 1);
+      acc[i % NBW] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[i % RING], __builtin_bit_cast(bf16x8, a_cur[i / NBW]),
+                                                              acc[i % NBW], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- epilogue: lane holds channels n0 + (cg*NBW + nb)*16 + nq .. +3 of token m.  Outputs go through
+    // a per-wave LDS tile so that global stores are whole 16-B chunks of token rows (8-B stores scattered
+    // over 16 rows per instruction ran the write-heavy launches at 2.2-2.8 TB/s)
+    const long mt0 = (long)t * ROWS_T + rg * 16;          // first token of this wave's tile
+    const int c0 = n0 + cg * NBW * 16;                    // first channel of this wave's columns
+    auto flush = [&](bf16raw* dst, long ld) {              // staged [16][NBW*16] tile -> dst rows
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      constexpr int CPR = NBW * 2;                          // 16-B chunks per row
+#pragma unroll
+      for (int c = lane; c < 16 * CPR; c += 64) {
+        const int r = c / CPR, ch = (c % CPR) * 8;
+        const uint4 u = *reinterpret_cast<const uint4*>(stg + r * SS + ch);
+        if (mt0 + r < g.M && c0 + ch < g.N) *reinterpret_cast<uint4*>(dst + (mt0 + r) * ld + c0 + ch) = u;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // reads done before the tile is rewritten
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto put = [&](int nb, const float (&v)[4], bf16raw* dst, long ld) {
+      uint2 o;
+      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      if (staged) *reinterpret_cast<uint2*>(stg + mrow * SS + nb * 16 + nq) = o;
+      else if (mok && c0 + nb * 16 + nq < g.N) *reinterpret_cast<uint2*>(dst + m * ld + c0 + nb * 16 + nq) = o;
+    };
+    if (g.act == 1 && aux) {        // the pre-activation (GELU backward input) first
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) {
+        const int n = c0 + nb * 16 + nq;
+        float v[4] = {acc[nb][0], acc[nb][1], acc[nb][2], acc[nb][3]};
+        if (bias && n < g.N) {
+          const uint2 b = *reinterpret_cast<const uint2*>(bias + n);
+          v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
+          v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
+        }
+        put(nb, v, aux, g.ldaux);
+      }
+      if (staged) flush(aux, g.ldaux);
+    }
+    {
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) {
+        const int n = c0 + nb * 16 + nq;
+        const bool ok = mok && n < g.N;
+        float v[4] = {acc[nb][0], acc[nb][1], acc[nb][2], acc[nb][3]};
+        if (bias && n < g.N) {
+          const uint2 b = *reinterpret_cast<const uint2*>(bias + n);
+          v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
+          v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
+        }
+        if (g.act == 1) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+        } else if (g.act == 2 && ok) {
+          const uint2 a = *reinterpret_cast<const uint2*>(aux + m * g.ldaux + n);
+          v[0] *= dgelu_f(__uint_as_float(a.x << 16)); v[1] *= dgelu_f(__uint_as_float(a.x & 0xffff0000u));
+          v[2] *= dgelu_f(__uint_as_float(a.y << 16)); v[3] *= dgelu_f(__uint_as_float(a.y & 0xffff0000u));
+        }
+        if (res && ok) {
+          const uint2 r = *reinterpret_cast<const uint2*>(res + m * g.ldr + n);
+          v[0] += __uint_as_float(r.x << 16); v[1] += __uint_as_float(r.x & 0xffff0000u);
+          v[2] += __uint_as_float(r.y << 16); v[3] += __uint_as_float(r.y & 0xffff0000u);
+        }
+        put(nb, v, C, g.ldc);
+        if (nb % 4 == 3) __builtin_amdgcn_sched_barrier(0);   // bound the epilogue loads hoisted ahead
+      }
+      if (staged) flush(C, g.ldc);
+    }
+  };
+
+  // the next tile's A fragments are in flight while this tile computes (deeper register queues of A
+  // tiles spilled: the unrolled process() bodies get interleaved by the scheduler)
+  int t = blockIdx.x / nslices;
+  uint4 a_nxt[KC];
+  if (t < ntiles) load_a(t, a_nxt);
+  for (; t < ntiles; t += stride) {
+    uint4 cur[KC];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) cur[kc] = a_nxt[kc];
+    if (t + stride < ntiles) load_a(t + stride, a_nxt);
+    process(t, cur);
+  }
+}
+
+template <int KC, int NBW, int NSPLIT>
+void launch_wres(const dfk_gemm_args& g, int nslices, hipStream_t s) {
+  // persistent grid: as many 8-wave workgroups per CU as the W slice's LDS allows (1 or 2), a multiple
+  // of the slice count so every workgroup keeps one slice for its whole life
+  constexpr int per_cu = wres_two_per_cu<KC, NBW, NSPLIT>() ? 2 : 1;
+  const int ntiles = dfk_cdiv(g.M, 16 * (8 / NSPLIT));
+  const int per = std::max(1, std::min(ntiles, 256 * per_cu / nslices));
+  hipLaunchKernelGGL((wres_kernel<KC, NBW, NSPLIT>), dim3(per * nslices), dim3(NT), 0, s, g, nslices, ntiles);
+}
+
+bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
+
+}  // namespace
+
+// 1 = launched, 0 = not applicable (caller runs the tiled GEMM), < 0 = launch error
+int dfk_wres_try(const dfk_gemm_args& g, hipStream_t s) {
+  static const bool off = getenv("DFK_WRES") && atoi(getenv("DFK_WRES")) == 0;
+  if (off) return 0;
+  if (g.dtype != DFK_BF16 || g.a_kmajor || g.c_f32 || g.atomic || g.splitk != 1 || g.rowsum) return 0;
+  if (g.nz0 != 1 || g.nz1 != 1 || g.a.conv_cg > 0 || g.b.conv_cg > 0 || g.beta != 0.f) return 0;
+  if (g.M < 16384 || g.K % 32 || g.K > 384 || g.N % 4) return 0;
+  if (g.act == 2 && !g.aux) return 0;
+  if (g.a.ld % 8 || ((uintptr_t)g.a.ptr & 15) || g.b.ld % 8 || ((uintptr_t)g.b.ptr & 15)) return 0;
+  if (g.ldc % 4 || !al8(g.c) || (g.bias && !al8(g.bias)) || (g.residual && (g.ldr % 4 || !al8(g.residual))) ||
+      (g.aux && (g.ldaux % 4 || !al8(g.aux))))
+    return 0;
+  if (g.b_kmajor && g.N % 8) return 0;
+  const int KC = g.K / 32;
+  // widest slice (fewest A re-reads) that fits WRES_LIMIT, then the least padding among equal counts
+  int best = 0, best_sl = 1 << 30, best_waste = 1 << 30;
+  for (int bn : {288, 192, 96}) {
+    if (bn * g.K > WRES_LIMIT) continue;
+    const int sl = dfk_cdiv(g.N, bn), waste = sl * bn - g.N;
+    if (sl < best_sl || (sl == best_sl && waste < best_waste)) { best = bn; best_sl = sl; best_waste = waste; }
+  }
+  if (!best || best_sl > 8) return 0;
+  // slice = NSPLIT column groups of NBW*16 channels: 96 (6x1), 192 (6x2), 288 (9x2)
+#define WRES_CASE(kc, nbw, ns) \
+  if (KC == kc && best == nbw * 16 * ns) { launch_wres<kc, nbw, ns>(g, best_sl, s); DFK_CHECK_LAUNCH(); return 1; }
+  WRES_CASE(3, 9, 2) WRES_CASE(4, 9, 2)
+  WRES_CASE(3, 6, 2) WRES_CASE(4, 6, 2) WRES_CASE(6, 6, 2) WRES_CASE(8, 6, 2)
+  WRES_CASE(3, 6, 1) WRES_CASE(4, 6, 1) WRES_CASE(6, 6, 1) WRES_CASE(8, 6, 1) WRES_CASE(9, 6, 1) WRES_CASE(12, 6, 1)
+#undef WRES_CASE
+  return 0;
+}

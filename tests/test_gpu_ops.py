@@ -54,6 +54,32 @@ def test_linear_fwd_bwd(dt, M, N, Kd):
     assert rel(db2, dy.float().sum(0)) < tol(dt)
 
 
+@pytest.mark.parametrize("M,N,Kd", [(20000, 288, 96), (16500, 96, 384), (17000, 384, 96), (16385, 576, 192),
+                                    (20000, 512, 128), (16400, 192, 768), (16384, 96, 288)])
+def test_linear_weight_resident(M, N, Kd):
+    """bf16 Linears with >= 16k tokens and a small weight run on the weight-resident streaming kernel
+    (wres.hip): ragged last row tile, several / partial column slices, every epilogue (bias, GELU with
+    the pre-activation saved, dGELU, residual) and the transposed-weight dX form."""
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(2)
+    x = torch.randn(M, Kd, device=DEV, generator=g).to(dt)
+    w = (torch.randn(N, Kd, device=DEV, generator=g) / math.sqrt(Kd)).to(dt)
+    b = torch.randn(N, device=DEV, generator=g).to(dt)
+    r = torch.randn(M, N, device=DEV, generator=g).to(dt)
+    pre = x.float() @ w.float().t() + b.float()
+    assert rel(K.linear(x, w, b, residual=r), pre + r.float()) < tol(dt)
+    aux = torch.empty(M, N, device=DEV, dtype=dt)
+    y = K.linear(x, w, b, act=1, aux=aux)
+    assert rel(aux, pre) < tol(dt)
+    assert rel(y, torch.nn.functional.gelu(pre)) < tol(dt)
+    dy = torch.randn(M, N, device=DEV, generator=g).to(dt)
+    assert rel(K.linear_dx(dy, w), dy.float() @ w.float()) < tol(dt)
+    # fc2-style dX with the GELU derivative of a saved pre-activation: (dy W) * gelu'(aux2)
+    aux2 = torch.randn(M, Kd, device=DEV, generator=g).to(dt)
+    ref2 = (dy.float() @ w.float()) * torch.func.grad(lambda t: torch.nn.functional.gelu(t).sum())(aux2.float())
+    assert rel(K.linear_dx(dy, w, act=2, aux=aux2), ref2) < tol(dt)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("rows,C", [(1000, 96), (33, 768), (17, 3072), (5, 512), (1001, 192), (77, 384), (9, 128),
                                     (13, 1536), (3, 1024), (29, 256)])
