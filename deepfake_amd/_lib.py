@@ -82,6 +82,8 @@ SIGNATURES = {
     "dfk_w2v_conv0_fwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP],
     "dfk_w2v_conv0_bwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _VP, _VP, _VP, _VP],
     "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP],
+    "dfk_frame_normalize": [_VP, _VP, _I64, _I32, _I32, C.POINTER(C.c_float), C.POINTER(C.c_float), _VP],
+    "dfk_wave_normalize": [_VP, _VP, _I64, _I64, _F, _VP],
 }
 
 _lib = None

@@ -299,6 +299,31 @@ def cast(x, dtype):
     return y
 
 
+def frame_normalize(frames_u8, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)):
+    """uint8 [..., H, W, 3] decoded RGB frames -> fp32 [..., 3, H, W] = (x/255 - mean) / std
+    (T.ToTensor + T.Normalize, data/data_process.py:55-69)."""
+    import ctypes
+    *lead, H, W, c3 = frames_u8.shape
+    if c3 != 3 or frames_u8.dtype != torch.uint8:
+        raise ValueError("frame_normalize expects uint8 [..., H, W, 3]")
+    x = frames_u8.contiguous()
+    out = torch.empty(*lead, 3, H, W, device=x.device, dtype=torch.float32)
+    m = (ctypes.c_float * 3)(*mean)
+    s = (ctypes.c_float * 3)(*std)
+    L.check(L.lib().dfk_frame_normalize(L.ptr(x), L.ptr(out), x.numel() // (3 * H * W), H, W, m, s, L.stream()),
+            "frame_normalize")
+    return out
+
+
+def wave_normalize(wave, eps=1e-7):
+    """[B, S] fp32 (zero-padded rows) -> per-row (x - mean) / sqrt(var + eps)."""
+    x = wave.float().contiguous()
+    out = torch.empty_like(x)
+    L.check(L.lib().dfk_wave_normalize(L.ptr(x), L.ptr(out), x.shape[0], x.shape[1], float(eps), L.stream()),
+            "wave_normalize")
+    return out
+
+
 def sgd_step(param, grad, buf, shadow, lr, momentum, wd, first, lr_dev=None):
     L.check(L.lib().dfk_sgd_step(L.ptr(param), L.ptr(grad), L.ptr(buf), L.ptr(shadow) if shadow is not None else None,
                                  param.numel(), L.ptr(lr_dev) if lr_dev is not None else None, float(lr),

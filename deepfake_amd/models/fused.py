@@ -45,14 +45,50 @@ CONFIGS = {
 }
 
 
-def build_fused(cfg, args=None, w2v_config=W2V_CONFIG, compute_dtype=torch.float32):
+def build_fused(cfg, args=None, w2v_config=W2V_CONFIG, compute_dtype=torch.float32, regularize=False):
+    """The north-star fused model.  regularize=False (parity / default): every dropout, DropPath,
+    SpecAugment and LayerDrop off (Q12).  regularize=True: the reference's training regularisers — VST
+    drop_path_rate 0.2 (SwinTransformer3D default, video_swin_transformer.py:500), SwinV2 0.1
+    (swin_transformer2d.py:506), the wav2vec2-base checkpoint config's dropouts / LayerDrop /
+    mask_time_prob, Audio2D's dropout (args.swin_drop) and the head's (args.classify_drop)."""
     if isinstance(cfg, str):
         cfg = CONFIGS[cfg]
     args = args or types.SimpleNamespace(soft=0.01, classify_drop=0.0, swin_drop=0.0)
-    vst = SwinTransformer3D(**cfg["vst"])
-    mel = SwinTransformerV2(**cfg["mel"])
-    wcfg = Wav2Vec2Config.from_json_file(w2v_config, num_hidden_layers=cfg["w2v_layers"]).deterministic()
+    vkw, mkw = dict(cfg["vst"]), dict(cfg["mel"])
+    if regularize:
+        vkw["drop_path_rate"], mkw["drop_path_rate"] = 0.2, 0.1
+    vst = SwinTransformer3D(**vkw)
+    mel = SwinTransformerV2(**mkw)
+    wcfg = Wav2Vec2Config.from_json_file(w2v_config, num_hidden_layers=cfg["w2v_layers"])
+    if not regularize:
+        wcfg = wcfg.deterministic()
     pa = Audio2D(args, Wav2Vec2Model(wcfg), num_classes=1, use_feat=True)
     m = FusionModel(args, VSTFeat(vst), mel, pa, out_dim=1, video_dim=cfg["video_dim"], audio_dim=cfg["audio_dim"],
                     paudio_dim=768)
     return set_compute_dtype(m, compute_dtype)
+
+
+def build_model(args, compute_dtype=torch.float32):
+    """train.py:29-49 model choice by --modality, with the north-star video slot:
+      fused  -> FusionModel(VSTFeat(SwinTransformer3D), SwinTransformerV2(use_feat), Audio2D(wav2vec2))
+      video  -> VideoClassifier (SwinTransformer3D + mean-pool Mlp head, video_swin_transformer.py:688-793)
+      audio  -> SwinTransformerV2(num_classes=1, 128; 2,2,18,2) (train.py:35)
+      paudio -> Audio2D(wav2vec2-base) (train.py:39-41)
+    Shapes come from --config; regularisers follow --deterministic."""
+    from .video_swin_transformer import VideoClassifier
+    cfg = CONFIGS[getattr(args, "config", "c2")]
+    reg = not getattr(args, "deterministic", False)
+    if args.modality == "fused":
+        return build_fused(cfg, args, compute_dtype=compute_dtype, regularize=reg)
+    if args.modality == "video":
+        vkw = dict(cfg["vst"], drop_path_rate=0.2 if reg else 0.0)
+        return set_compute_dtype(VideoClassifier(args, SwinTransformer3D(**vkw), num_classes=1), compute_dtype)
+    if args.modality == "audio":
+        mkw = dict(cfg["mel"], use_feat=False, drop_path_rate=0.1 if reg else 0.0)
+        return set_compute_dtype(SwinTransformerV2(**mkw), compute_dtype)
+    if args.modality == "paudio":
+        wcfg = Wav2Vec2Config.from_json_file(W2V_CONFIG, num_hidden_layers=cfg["w2v_layers"])
+        if not reg:
+            wcfg = wcfg.deterministic()
+        return set_compute_dtype(Audio2D(args, Wav2Vec2Model(wcfg), num_classes=1), compute_dtype)
+    raise ValueError(f"unknown modality {args.modality!r}")

@@ -274,6 +274,49 @@ class SwinTransformer3D(nn.Module):
         return self
 
 
+class PoolingMLP(nn.Module):
+    """video_swin_transformer.py:688-731 with PoolingMethod 'mean' (the 'Attention' variant's
+    TransformerEncoder head is not built): classify = Mlp(mean over D,H,W), feat = mean over H,W -> [B,D,C].
+    Takes the backbone's channels-last tokens [B, D, H, W, C]."""
+
+    def __init__(self, args, in_feature, num_hidden=128, num_classes=2, PoolingMethod='mean'):
+        super().__init__()
+        if PoolingMethod not in (None, 'mean'):
+            raise NotImplementedError("PoolingMLP: only the 'mean' pooling is built")
+        self.Pooling = 'mean'
+        self.mlp = Mlp(in_feature, num_hidden, num_classes, drop=getattr(args, "classify_drop", 0.0))
+
+    def forward(self, t):
+        B, D, H, W, C = t.shape
+        classify = self.mlp(Fn.RowMeanFn.apply(t.reshape(-1, C), B))
+        feat = t.float().mean(dim=(2, 3))
+        return classify.squeeze(), feat
+
+
+class VideoClassifier(nn.Module):
+    """video_swin_transformer.py:734-793 (video modality): SwinTransformer3D -> PoolingMLP -> sigmoid.
+    Returns the probability only: the reference returns (prob, feat[B,D,C]), a tuple its own Trainer's
+    BCELoss cannot take (src/trainer.py:132).  The reference builds Swin with depths 2,2,18,2 / window 8x7x7 /
+    drop_path 0.1 and loads args.video_pretrained_dir unconditionally (Q8, absent here): `backbone`
+    overrides the architecture, and no checkpoint is read.  Input [B,T,C,H,W] as the dataset yields
+    it (the reference never permutes, Q8)."""
+
+    def __init__(self, args, backbone=None, num_classes=2, num_hiddens=None):
+        super().__init__()
+        self.videoSwinT = backbone or SwinTransformer3D(embed_dim=96, depths=[2, 2, 18, 2], num_heads=[3, 6, 12, 24],
+                                                        patch_size=(2, 4, 4), window_size=(8, 7, 7),
+                                                        drop_path_rate=0.1, patch_norm=True)
+        self.pool = getattr(args, "video_pool", None)
+        self.classsifier = PoolingMLP(args, self.videoSwinT.num_features,
+                                      num_hiddens or getattr(args, "num_hiddens", 128), num_classes, self.pool)
+        self.prob = nn.Sigmoid()
+
+    def forward(self, x):
+        t = self.videoSwinT.forward_tokens(x, layout="btchw")
+        classify, feat = self.classsifier(t)
+        return self.prob(classify.float())
+
+
 class VSTFeat(nn.Module):
     """Video slot of the north-star FusionModel: the dataset's
     [B,T,C,H,W] clip read in place (strided im2col, no permute copy) ->

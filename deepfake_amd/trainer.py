@@ -27,12 +27,32 @@ from .params import ParamStore
 from .utils import AverageMeter, Logger
 
 
+def pad_longest(waves):
+    """The processor's padding='longest' (src/trainer.py:258): zero-pad every waveform of the batch to the
+    longest one -> [B, S] fp32 (host)."""
+    if torch.is_tensor(waves):
+        return waves.float()
+    arrs = [torch.as_tensor(w, dtype=torch.float32).reshape(-1) for w in waves]
+    S = max(a.numel() for a in arrs)
+    out = torch.zeros(len(arrs), S, dtype=torch.float32)
+    for i, a in enumerate(arrs):
+        out[i, :a.numel()] = a
+    return out
+
+
 def normalize_wave(w):
-    """Wav2Vec2FeatureExtractor zero-mean / unit-variance (HF feature_extraction_wav2vec2.py:94-95),
-    on device, for equal-length clips (src/trainer.py:258)."""
-    m = w.mean(-1, keepdim=True)
-    v = w.var(-1, keepdim=True, unbiased=False)
-    return (w - m) / torch.sqrt(v + 1e-7)
+    """Wav2Vec2FeatureExtractor zero-mean / unit-variance (HF feature_extraction_wav2vec2.py:94-95) of every
+    zero-padded row, whole row included (no attention mask, Q13) — on the GPU (dfk_wave_normalize)."""
+    from . import kernels as K
+    return K.wave_normalize(w)
+
+
+def prepare_video(video, device):
+    """Frames to the device: fp32 transform output as is; decoded uint8 RGB frames [B,T,H,W,3] normalised on
+    the GPU (T.ToTensor + T.Normalize, data/data_process.py:55-69) -> [B,T,3,H,W]."""
+    from . import kernels as K
+    v = video.to(device, non_blocking=True)
+    return K.frame_normalize(v) if v.dtype == torch.uint8 else v
 
 
 class TrainStep:
@@ -185,17 +205,39 @@ class Trainer:
             torch.save({"epoch": epoch, "checkpoint": self.model_s.state_dict(),
                         "optimizer": self.optimizer.state_dict()}, path)
 
-    def _prep(self, batch):
-        feat, label = batch[0], batch[1]
+    def _features(self, feat):
+        """src/trainer.py:250-262: the batch's features on the device, waveforms padded to the longest and
+        normalised (the processor), frames normalised when they arrive as decoded uint8."""
         if self.modality == "fused":
-            video, mel, wave = feat["Video"], feat["Audio"], feat["PAudio"]
-            if isinstance(wave, (list, tuple)):
-                wave = torch.stack([torch.as_tensor(w) for w in wave])
-            wave = normalize_wave(wave.to(self.device, non_blocking=True).float())
-            feature = (video.to(self.device, non_blocking=True), mel.to(self.device, non_blocking=True), wave)
-        else:
-            feature = feat.to(self.device, non_blocking=True)
-        return feature, label.to(self.device, non_blocking=True)
+            wave = normalize_wave(pad_longest(feat["PAudio"]).to(self.device, non_blocking=True))
+            return (prepare_video(feat["Video"], self.device), feat["Audio"].to(self.device, non_blocking=True), wave)
+        if self.modality == "paudio":
+            return normalize_wave(pad_longest(feat).to(self.device, non_blocking=True))
+        if self.modality == "video":
+            return prepare_video(feat, self.device)
+        return feat.to(self.device, non_blocking=True)
+
+    def _prep(self, batch):
+        return self._features(batch[0]), batch[1].to(self.device, non_blocking=True)
+
+    def submit(self, dataloader=None, path="prediction.csv"):
+        """Inference over the test split (src/submit.py:79-120, SubmitCtl.submit): appends
+        'filename,probability' rows to `path`; returns {filename: probability}."""
+        dataloader = dataloader or self.dataset.test_dataloader()
+        self.model.eval()
+        res = {}
+        with torch.no_grad(), open(path, "a") as f:
+            for iter_id, (feat, names) in enumerate(dataloader):
+                out = self.model(self._features(feat)).float().reshape(-1).cpu()
+                for name, v in zip(names, out.numpy()):
+                    f.write("{0},{1}\n".format(name, v))
+                    res[name] = float(v)
+                if iter_id % self.log_step == 0:
+                    self.logger("|step {:4d} |total {:4d}| Rate% {:.3f}".format(iter_id, len(dataloader),
+                                                                               iter_id / len(dataloader) * 100))
+        self.logger("Test Score Prediction Done")
+        self.model.train()
+        return res
 
     def run_batch(self, feature, label, gpu_log=None):
         """Forward + loss + accuracy (src/trainer.py:124-148); no host sync here."""
@@ -218,6 +260,7 @@ class Trainer:
                 stat.update(r["loss"].item())
                 t += 1
         self.logger(f"Phase:val, Avg Loss:{stat.avg}")
+        self.model.train()
         return t
 
     def train(self):

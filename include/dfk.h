@@ -222,6 +222,17 @@ int dfk_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf1
                  const float* lr_dev, float lr, float momentum, float weight_decay, int first_step,
                  hipStream_t stream);
 
+/* Frame normalisation on the device: T.ToTensor() + T.Normalize(mean, std) of
+ * data/data_process.py:55-69 on decoded RGB frames (src/utils.py:22-39): src uint8 [frames, H, W, 3]
+ * -> dst fp32 [frames, 3, H, W], (x/255 - mean[c]) / std[c] in fp32 (bit-exact to torchvision).
+ * mean3 / std3 are HOST arrays of 3 floats.  Requires H*W % 4 == 0, dst 16-B aligned. */
+int dfk_frame_normalize(const uint8_t* src, float* dst, int64_t frames, int32_t H, int32_t W, const float* mean3,
+                        const float* std3, hipStream_t stream);
+/* Waveform normalisation on the device: Wav2Vec2FeatureExtractor zero_mean_unit_var_norm
+ * (transformers feature_extraction_wav2vec2.py:94-95, called at src/trainer.py:258) of every row of a
+ * zero-padded [B, S] batch (no attention mask, Q13): y = (x - mean) / sqrt(var + eps), eps = 1e-7. */
+int dfk_wave_normalize(const float* x, float* y, int64_t B, int64_t S, float eps, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -309,9 +309,41 @@ def case_state_keys():
     print("state_keys:", {k: len(v) for k, v in out.items()})
 
 
+def case_config_flags():
+    """Every flag of the reference's config.py:3-45 (dest, option strings, type, default, action) from
+    its own argparse parser, for the entry-surface test of config.py."""
+    import argparse
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("ref_config", os.path.join("/root/reference", "config.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    captured = {}
+    orig = argparse.ArgumentParser.parse_args
+
+    def grab(self, args=None, namespace=None):
+        captured["parser"] = self
+        return orig(self, [], namespace)
+    argparse.ArgumentParser.parse_args = grab
+    try:
+        mod.get_opt()
+    finally:
+        argparse.ArgumentParser.parse_args = orig
+    flags = []
+    for a in captured["parser"]._actions:
+        if a.dest == "help":
+            continue
+        flags.append(dict(dest=a.dest, options=list(a.option_strings), type=getattr(a.type, "__name__", None),
+                          default=a.default, action=type(a).__name__))
+    with open(os.path.join(HERE, "config_flags.json"), "w") as f:
+        json.dump(flags, f, indent=1)
+    print("config flags:", len(flags))
+
+
 if __name__ == "__main__":
     only = sys.argv[1:]
     for fn in [case_window_attention, case_block, case_patch_embed_merge, case_vst_c1, case_w2v, case_head,
-               case_fused_c1, case_block_c2, case_mel_c2, case_fused_c1_grads, case_fused_c2, case_state_keys]:
+               case_fused_c1, case_block_c2, case_mel_c2, case_fused_c1_grads, case_fused_c2, case_state_keys,
+               case_config_flags]:
         if not only or fn.__name__ in only:
             fn()
