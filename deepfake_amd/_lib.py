@@ -51,6 +51,14 @@ class WattnBwdArgs(C.Structure):
                 ("dpad_v", C.c_void_p), ("ld_dqkv", C.c_int64), ("ld_dout", C.c_int64), ("ws", C.c_void_p)]
 
 
+class PatchEmbedArgs(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("sb", C.c_int64), ("sc", C.c_int64), ("st", C.c_int64), ("sh", C.c_int64),
+                ("sw", C.c_int64), ("B", C.c_int32), ("T", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
+                ("C", C.c_int32), ("w", C.c_void_p), ("b", C.c_void_p), ("ln_w", C.c_void_p), ("ln_b", C.c_void_p),
+                ("eps", C.c_float), ("out", C.c_void_p), ("mean", C.c_void_p), ("rstd", C.c_void_p),
+                ("dw", C.c_void_p), ("db", C.c_void_p), ("dln_w", C.c_void_p), ("dln_b", C.c_void_p)]
+
+
 class Im2colArgs(C.Structure):
     _fields_ = [("sb", C.c_int64), ("sc", C.c_int64), ("st", C.c_int64), ("sh", C.c_int64), ("sw", C.c_int64),
                 ("B", C.c_int32), ("cin", C.c_int32), ("T", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
@@ -84,6 +92,8 @@ SIGNATURES = {
     "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP],
     "dfk_frame_normalize": [_VP, _VP, _I64, _I32, _I32, C.POINTER(C.c_float), C.POINTER(C.c_float), _VP],
     "dfk_wave_normalize": [_VP, _VP, _I64, _I64, _F, _VP],
+    "dfk_patch_embed_fwd": [C.POINTER(PatchEmbedArgs), _VP],
+    "dfk_patch_embed_bwd": [C.POINTER(PatchEmbedArgs), _VP, _VP],
 }
 
 _lib = None

@@ -386,6 +386,37 @@ class CosineQKFn(torch.autograd.Function):
         return dqkv, ds, None, None
 
 
+class PatchEmbedLNFn(torch.autograd.Function):
+    """Fused PatchEmbed3D pad + Conv3d(2x4x4) + LayerNorm in bf16 (video_swin_transformer.py:446-458):
+    dfk_patch_embed_fwd reads the fp32 clip once and writes the normalised bf16 tokens once; the backward
+    recomputes the conv from the clip (nothing but the LN statistics is saved) and returns the four
+    parameter gradients.  -> token-major [B*Do*Ho*Wo, C] bf16."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, ln_w, ln_b, layout, eps):
+        dt = torch.bfloat16
+        W = compute_weight(weight, dt).reshape(weight.shape[0], -1)
+        Bc, G, Bt = (compute_weight(t, dt) for t in (bias, ln_w, ln_b))
+        y, mean, rstd, grid = K.patch_embed_fwd(x, layout, W, Bc, G, Bt, eps)
+        for i, p in enumerate((weight, bias, ln_w, ln_b)):
+            grad_use(ctx, 1 + i, p)
+        ctx.save_for_backward(x, weight, bias, ln_w, ln_b, mean, rstd)
+        ctx.layout, ctx.eps = layout, eps
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias, ln_w, ln_b, mean, rstd = ctx.saved_tensors
+        dt = torch.bfloat16
+        W = compute_weight(weight, dt).reshape(weight.shape[0], -1)
+        Bc, G, Bt = (compute_weight(t, dt) for t in (bias, ln_w, ln_b))
+        dw, db, dg, dbt = grad_sink(weight), grad_sink(bias), grad_sink(ln_w), grad_sink(ln_b)
+        K.patch_embed_bwd(x, ctx.layout, W, Bc, G, Bt, ctx.eps, mean, rstd, dy.contiguous(), dw.view(dw.shape[0], -1),
+                          db, dg, dbt)
+        return (None, grad_done(weight, dw), grad_done(bias, db), grad_done(ln_w, dg), grad_done(ln_b, dbt), None,
+                None)
+
+
 class PatchEmbedFn(torch.autograd.Function):
     """Conv with kernel == stride as im2col + GEMM (+bias): PatchEmbed3D.proj
     (video_swin_transformer.py:436,453) / SwinV2 PatchEmbed.proj.  Returns

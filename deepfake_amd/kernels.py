@@ -245,6 +245,41 @@ def patch_im2col(x, layout, patch, out_dtype):
     return out, (B, Do, Ho, Wo)
 
 
+def patch_embed_args(x, layout, w, b, ln_w, ln_b, eps):
+    """dfk_patch_embed_args for a [B,T,3,H,W] ('btchw') or [B,3,T,H,W] ('bcthw') fp32 clip."""
+    a = L.PatchEmbedArgs()
+    if layout == "btchw":
+        B, T, _, H, W = x.shape
+        a.sb, a.st, a.sc, a.sh, a.sw = x.stride()
+    else:
+        B, _, T, H, W = x.shape
+        a.sb, a.sc, a.st, a.sh, a.sw = x.stride()
+    a.x = x.data_ptr()
+    a.B, a.T, a.H, a.W, a.C = B, T, H, W, w.shape[0]
+    a.w, a.b, a.ln_w, a.ln_b = w.data_ptr(), b.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr()
+    a.eps = float(eps)
+    return a, (B, -(-T // 2), -(-H // 4), -(-W // 4))
+
+
+def patch_embed_fwd(x, layout, w, b, ln_w, ln_b, eps):
+    """Fused pad + Conv3d(2x4x4) + LayerNorm -> (tokens [B*Do*Ho*Wo, C] bf16, mean, rstd, grid)."""
+    a, grid = patch_embed_args(x, layout, w, b, ln_w, ln_b, eps)
+    rows = grid[0] * grid[1] * grid[2] * grid[3]
+    out = torch.empty(rows, w.shape[0], device=x.device, dtype=torch.bfloat16)
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    a.out, a.mean, a.rstd = out.data_ptr(), mean.data_ptr(), rstd.data_ptr()
+    L.check(L.lib().dfk_patch_embed_fwd(a, L.stream()), "patch_embed_fwd")
+    return out, mean, rstd, grid
+
+
+def patch_embed_bwd(x, layout, w, b, ln_w, ln_b, eps, mean, rstd, dy, dw, db, dln_w, dln_b):
+    a, _ = patch_embed_args(x, layout, w, b, ln_w, ln_b, eps)
+    a.mean, a.rstd = mean.data_ptr(), rstd.data_ptr()
+    a.dw, a.db, a.dln_w, a.dln_b = dw.data_ptr(), db.data_ptr(), dln_w.data_ptr(), dln_b.data_ptr()
+    L.check(L.lib().dfk_patch_embed_bwd(a, L.ptr(dy), L.stream()), "patch_embed_bwd")
+
+
 def patch_merge(x, dims, reverse=False, out=None):
     """dims = (B, D, H, W) of the un-merged volume; x token-major rows (or merged rows when reverse)."""
     B, D, H, W = dims

@@ -204,6 +204,14 @@ class PatchEmbed3D(nn.Module):
         self.norm = norm_layer(embed_dim) if norm_layer is not None else None
         self.compute_dtype = torch.float32
 
+    def fused_ok(self, x):
+        """The fused bf16 kernel's geometry: 3 input channels, 2x4x4 patches, C in {96, 128}, LayerNorm,
+        an fp32 clip whose W stride is 1, <= 256 pixels per row (fp32 parity mode keeps the 3-pass path)."""
+        return (self.compute_dtype == torch.bfloat16 and self.norm is not None and self.in_chans == 3 and
+                self.patch_size == (2, 4, 4) and self.embed_dim in (96, 128) and x.dtype == torch.float32 and
+                x.stride(-1) == 1 and all(s % 4 == 0 for s in x.stride()[:-1]) and x.shape[-1] <= 256 and
+                x.data_ptr() % 16 == 0 and not getattr(self, "force_unfused", False))
+
     def tokens(self, x, layout="bcthw"):
         """-> channels-last [B, D', H', W', C] in the compute dtype."""
         if layout == "btchw":
@@ -212,6 +220,10 @@ class PatchEmbed3D(nn.Module):
             B, _, T, H, W = x.shape
         pd, ph, pw = self.patch_size
         Do, Ho, Wo = -(-T // pd), -(-H // ph), -(-W // pw)
+        if self.fused_ok(x):   # one pass: pad + Conv3d + LayerNorm (dfk_patch_embed_fwd)
+            y = Fn.PatchEmbedLNFn.apply(x, self.proj.weight, self.proj.bias, self.norm.weight, self.norm.bias, layout,
+                                        self.norm.eps)
+            return y.view(B, Do, Ho, Wo, self.embed_dim)
         y = Fn.PatchEmbedFn.apply(x, self.proj.weight, self.proj.bias, layout, self.patch_size, self.compute_dtype)
         if self.norm is not None:
             y = Fn.layer_norm(y, self.norm)

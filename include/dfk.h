@@ -177,6 +177,32 @@ typedef struct {
 int dfk_patch_im2col(const void* x, int x_dtype, void* out, int out_dtype, const dfk_im2col_args* a,
                      hipStream_t stream);
 
+/* Fused PatchEmbed3D (video_swin_transformer.py:420-460: pad + Conv3d(3->C, k = s = 2x4x4) + LayerNorm(C)),
+ * bf16 compute, one pass over the clip.  x fp32 clip, element strides sb..sw (sw == 1, others multiples of 4:
+ * [B,T,3,H,W] clips are read in place); w [C][96] bf16 (the Conv3d weight flattened), b, ln_w, ln_b [C] bf16;
+ * C in {96, 128}.  fwd: out [B*Do*Ho*Wo][C] bf16 normalised tokens, mean/rstd [tokens] fp32 (LN statistics of
+ * the fp32 conv output).  bwd (dy = d out, bf16): recomputes the conv from the clip and accumulates (+=, fp32)
+ * dw [C][96], db, dln_w, dln_b [C]; no input gradient. */
+typedef struct {
+  const void* x;
+  int64_t sb, sc, st, sh, sw;
+  int32_t B, T, H, W, C;
+  const void* w;
+  const void* b;
+  const void* ln_w;
+  const void* ln_b;
+  float eps;
+  void* out;
+  float* mean;
+  float* rstd;
+  float* dw;
+  float* db;
+  float* dln_w;
+  float* dln_b;
+} dfk_patch_embed_args;
+int dfk_patch_embed_fwd(const dfk_patch_embed_args* a, hipStream_t stream);
+int dfk_patch_embed_bwd(const dfk_patch_embed_args* a, const void* dy, hipStream_t stream);
+
 /* PatchMerging 2x2 gather (reverse=0) / its gradient scatter (reverse=1) on
  * channels-last [B*D, H, W, C] <-> [B*D*ceil(H/2)*ceil(W/2), 4C], order x0,x1,x2,x3 (Q7),
  * zero padding of odd H/W (video_swin_transformer.py:300-311). */

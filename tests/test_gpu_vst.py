@@ -72,6 +72,29 @@ def test_patch_embed(dt):
     grads(fx, m, tb)
 
 
+@pytest.mark.parametrize("shape,layout,C", [((2, 3, 8, 32, 32), "bcthw", 96), ((1, 32, 3, 224, 224), "btchw", 96),
+                                            ((1, 7, 3, 30, 44), "btchw", 128)])
+def test_patch_embed_fused_matches_unfused(shape, layout, C):
+    """The fused bf16 pad + Conv3d + LayerNorm kernel (dfk_patch_embed_fwd/bwd) against the three-pass
+    path (im2col -> GEMM -> LN) on the same inputs: C2 clip geometry in place ([B,T,3,H,W]), padded T/H/W,
+    Swin-B width.  Outputs and all four parameter gradients."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(*shape, generator=g).to(DEV)
+    outs = []
+    for fused in (True, False):
+        m = named_fill_(V.PatchEmbed3D((2, 4, 4), 3, C, norm_layer=torch.nn.LayerNorm), 17).to(DEV)
+        set_compute_dtype(m, torch.bfloat16)
+        m.force_unfused = not fused
+        assert m.fused_ok(x) == fused
+        y = m.tokens(x, layout)
+        y.backward(torch.randn(y.shape, generator=g.manual_seed(4)).to(DEV).to(y.dtype))
+        outs.append((y.float(), [p.grad.clone() for p in m.parameters()]))
+    (yf, gf), (yu, gu) = outs
+    assert (yf - yu).abs().max() / yu.abs().max() < 2e-2
+    for a, b in zip(gf, gu):
+        assert (a - b).abs().max() / b.abs().max() < 3e-2
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("c", GC.MERGE_CASES, ids=lambda c: c["name"])
 def test_patch_merging(dt, c):
