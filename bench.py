@@ -6,7 +6,10 @@ Workload (BASELINE.json configs[1], "C2"): Video Swin-T (depths 2,2,6,2, window
 over a 224x224 mel image + wav2vec2-base over 4 s @ 16 kHz + FusionModel head;
 B=8 clips per GPU; bf16 compute (fp32 master weights, fp32 softmax/LN stats);
 one step = forward + BCE + backward + RCCL gradient all-reduce + fused SGD
-(momentum 0.9, wd) — the whole step captured in one HIP graph and replayed
+(momentum 0.9, wd) with the reference's training regularisers on (VST DropPath
+0.2, SwinV2 DropPath 0.1, wav2vec2 feat-proj / hidden / activation / attention
+dropout 0.1, LayerDrop 0.1, SpecAugment mask_time_prob 0.05, Audio2D and head
+dropout 0.1; --deterministic turns them off) — the whole step captured in one HIP graph and replayed
 (the first warm-up step runs eagerly and captures; --eager replays nothing), with
 the video / mel / waveform trunks on three HIP streams inside the graph.
 Inputs are synthetic, generated on device and resident in HBM.
@@ -44,6 +47,7 @@ def parse():
     p.add_argument("--batch", type=int, default=8)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--eager", action="store_true", help="run the step eagerly instead of replaying its HIP graph")
+    p.add_argument("--deterministic", action="store_true", help="regularisers off (the parity setting)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=3)
     p.add_argument("--roofline-iters", type=int, default=20)
@@ -220,10 +224,12 @@ def main():
     from deepfake_amd.optim import FusedSGD
     from deepfake_amd.params import ParamStore
     from deepfake_amd.trainer import TrainStep
+    from deepfake_amd import rng
 
     cfg = CONFIGS[a.config]
     torch.manual_seed(1234)
-    model = build_fused(cfg, compute_dtype=dt).to(device)
+    rng.manual_seed(1234, rank)
+    model = build_fused(cfg, compute_dtype=dt, regularize=not a.deterministic).to(device)
     model.train()
     store = ParamStore(model, dt)
     bucketer = GradBucketer(store, bucket_mb=64.0)
@@ -273,7 +279,8 @@ def main():
             "config": {"workload": f"{a.config.upper()}: Swin-T video 32x224x224 (window 8x7x7) + SwinV2 mel 224 + "
                                    f"wav2vec2-base 4s@16kHz + FusionModel, full train step",
                        "global_batch": world * a.batch, "per_gpu_batch": a.batch,
-                       "parallelism": f"dp{world}", "hip_graph": not a.eager, "branch_streams": 3, "loss": round(lossv, 5)},
+                       "parallelism": f"dp{world}", "hip_graph": not a.eager, "branch_streams": 3,
+                       "regularisers": not a.deterministic, "loss": round(lossv, 5)},
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2) if train_gflop else None,
             "roofline": roof, "roofline_conv3d": roof_conv, "cpu_baseline": cpu,
         }

@@ -15,6 +15,11 @@ LIB_PATH = os.path.join(_HERE, "libdfk.so")
 F32, BF16 = 0, 1
 
 
+class Drop(C.Structure):
+    _fields_ = [("rng", C.c_void_p), ("mode", C.c_int32), ("site", C.c_int32), ("p", C.c_float),
+                ("group_rows", C.c_int32), ("shared", C.c_int32)]
+
+
 class View(C.Structure):
     _fields_ = [("ptr", C.c_void_p), ("ld", C.c_int64), ("bs0", C.c_int64), ("bs1", C.c_int64),
                 ("conv_cg", C.c_int32), ("conv_stride", C.c_int32), ("conv_pad", C.c_int32),
@@ -29,7 +34,7 @@ class GemmArgs(C.Structure):
                 ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("dtype", C.c_int32),
                 ("a_kmajor", C.c_int32), ("b_kmajor", C.c_int32), ("c_f32", C.c_int32), ("nz0", C.c_int32),
                 ("nz1", C.c_int32), ("splitk", C.c_int32), ("act", C.c_int32), ("atomic", C.c_int32),
-                ("beta", C.c_float), ("ws", C.c_void_p), ("rowsum", C.c_void_p)]
+                ("beta", C.c_float), ("ws", C.c_void_p), ("rowsum", C.c_void_p), ("drop", Drop)]
 
 
 class WattnArgs(C.Structure):
@@ -42,7 +47,7 @@ class WattnArgs(C.Structure):
                 ("fd", C.c_int32), ("fh", C.c_int32), ("fw", C.c_int32),
                 ("sd", C.c_int32), ("sh", C.c_int32), ("sw", C.c_int32),
                 ("heads", C.c_int32), ("hd", C.c_int32), ("dtype", C.c_int32), ("scale", C.c_float),
-                ("tab", C.c_void_p)]
+                ("tab", C.c_void_p), ("drop", Drop)]
 
 
 class WattnBwdArgs(C.Structure):
@@ -72,8 +77,9 @@ SIGNATURES = {
     "dfk_gemm": [C.POINTER(GemmArgs), _VP],
     "dfk_gemm_workspace": [C.POINTER(GemmArgs)],
     "dfk_colsum": [_VP, C.c_int, _I64, _I64, _I64, _VP, _VP],
-    "dfk_layernorm_fwd": [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, _F, C.c_int, _VP],
-    "dfk_layernorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, C.c_int, C.c_int, _VP, _VP],
+    "dfk_layernorm_fwd": [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, _F, C.c_int, _VP, C.POINTER(Drop), _VP],
+    "dfk_layernorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, C.c_int, C.c_int, _VP,
+                          C.POINTER(Drop), _VP],
     "dfk_layernorm_bwd_workspace": [_I64, _I32],
     "dfk_wattn_fwd": [C.POINTER(WattnArgs), _VP],
     "dfk_wattn_bwd": [C.POINTER(WattnBwdArgs), _VP],
@@ -89,7 +95,11 @@ SIGNATURES = {
     "dfk_cosine_qk_bwd": [_VP, _VP, _VP, _VP, _VP, _I64, C.c_int, C.c_int, C.c_int, _VP],
     "dfk_w2v_conv0_fwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP],
     "dfk_w2v_conv0_bwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _VP, _VP, _VP, _VP],
-    "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP],
+    "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP, _VP],
+    "dfk_dropout": [_VP, _VP, _I64, _I32, _I64, C.POINTER(Drop), C.c_int, _VP],
+    "dfk_bernoulli_flags": [C.POINTER(Drop), _I32, _VP, _VP],
+    "dfk_spec_augment_fwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _F, _I32, _I32, C.POINTER(Drop), C.c_int, _VP],
+    "dfk_spec_augment_bwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, C.c_int, _VP],
     "dfk_frame_normalize": [_VP, _VP, _I64, _I32, _I32, C.POINTER(C.c_float), C.POINTER(C.c_float), _VP],
     "dfk_wave_normalize": [_VP, _VP, _I64, _I64, _F, _VP],
     "dfk_patch_embed_fwd": [C.POINTER(PatchEmbedArgs), _VP],
@@ -134,6 +144,18 @@ def ptr(t):
     if not t.is_cuda:
         raise RuntimeError("deepfake_amd: tensors must be on the HIP device (no CPU fallback)")
     return C.c_void_p(t.data_ptr())
+
+
+def drop(spec, device):
+    """ctypes dfk_drop for a rng.Drop spec tuple (mode, site, p, group_rows, shared), or None."""
+    if spec is None:
+        return None
+    from . import rng
+    d = Drop()
+    d.rng = rng.state(device).data_ptr()
+    d.mode, d.site, d.p, d.group_rows, d.shared = int(spec[0]), int(spec[1]), float(spec[2]), int(spec[3]), \
+        int(spec[4])
+    return d
 
 
 def dt(t):

@@ -72,6 +72,43 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---- dropout masks (dfk_drop, include/dfk.h): counter-based hash of (seed, step, site, row, col) ----
+__device__ __forceinline__ uint32_t dfk_fmix(uint32_t h) {   // murmur3 finaliser
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+struct DropCtx {
+  uint32_t key, thr;   // per-launch key; drop iff (hash >> 8) < thr
+  float scale;         // 1 / (1 - p)
+  int mode, grows;
+};
+__device__ __forceinline__ DropCtx drop_ctx(const dfk_drop& d) {
+  DropCtx c;
+  c.mode = d.rng ? d.mode : 0;
+  c.key = 0; c.thr = 0; c.scale = 1.f; c.grows = d.group_rows > 0 ? d.group_rows : 1;
+  if (c.mode) {
+    const uint64_t seed = (uint64_t)d.rng[d.shared ? 2 : 0], step = (uint64_t)d.rng[1];
+    uint32_t h = dfk_fmix((uint32_t)seed ^ 0x9e3779b9u);
+    h = dfk_fmix(h ^ (uint32_t)(seed >> 32));
+    h = dfk_fmix(h + (uint32_t)step * 0x85ebca77u);
+    h = dfk_fmix(h ^ (uint32_t)(step >> 32));
+    c.key = dfk_fmix(h + (uint32_t)d.site * 0xc2b2ae3du);
+    c.thr = (uint32_t)(d.p * 16777216.f);
+    c.scale = 1.f / (1.f - d.p);
+  }
+  return c;
+}
+// element (row, col) draw of mode 1; group draw (row / grows) of mode 2
+__device__ __forceinline__ uint32_t drop_hash(const DropCtx& c, long row, long col) {
+  if (c.mode == 2) return dfk_fmix(c.key ^ dfk_fmix((uint32_t)(row / c.grows) + 0x6a09e667u));
+  const uint32_t h = dfk_fmix(c.key + (uint32_t)row * 0x9e3779b1u);
+  return dfk_fmix(h ^ ((uint32_t)col * 0x85ebca77u + 0x165667b1u));
+}
+__device__ __forceinline__ float drop_mul(const DropCtx& c, long row, long col) {
+  if (!c.mode) return 1.f;
+  return (drop_hash(c, row, col) >> 8) >= c.thr ? c.scale : 0.f;
+}
+
 #define DFK_CHECK_LAUNCH() \
   do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
 

@@ -175,6 +175,16 @@ __device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1
     if (full) ld8<T>(ap, a8); else for (int e = 0; e < ncol; ++e) a8[e] = ldf<T>(ap + e);
     for (int e = 0; e < 8; ++e) v[e] *= dgelu_f(a8[e]);
   }
+  if (g.drop.mode && g.drop.rng) {   // dropout / DropPath of the branch output (before the residual add)
+    const DropCtx dc = drop_ctx(g.drop);
+    const long rr = row + (long)(z0 * g.nz1 + z1) * g.M;
+    if (dc.mode == 2) {
+      const float m = drop_mul(dc, rr, 0);
+      for (int e = 0; e < 8; ++e) v[e] *= m;
+    } else {
+      for (int e = 0; e < 8; ++e) v[e] *= drop_mul(dc, rr, col0 + e);
+    }
+  }
   if (res) {
     const T* rp = res + (long)row * g.ldr + col0;
     if (full) { float r8[8]; ld8<T>(rp, r8); for (int e = 0; e < 8; ++e) v[e] += r8[e]; }
@@ -493,6 +503,7 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   if (g.atomic && (!g.c_f32 || g.bias || g.residual || g.act)) return DFK_EINVAL;
   if (g.act && g.act != 1 && !g.aux) return DFK_EINVAL;
   if (g.rowsum && (g.nz0 != 1 || g.nz1 != 1 || !g.a_kmajor || !g.b_kmajor)) return DFK_EINVAL;
+  if (g.drop.mode && (g.c_f32 || g.atomic || !g.drop.rng || !(g.drop.p >= 0.f && g.drop.p < 1.f))) return DFK_EINVAL;
   if (g.M <= 0 || g.N <= 0) return 0;
   if constexpr (sizeof(T) == 2) {
     const int w = dfk_wres_try(g, s);     // huge-M / small-weight Linears: weight-resident streaming kernel

@@ -54,7 +54,8 @@ __device__ __forceinline__ float group_sum(float v) {
 template <typename T, int L, int V>
 __global__ __launch_bounds__(256) void ln_fwd(const T* __restrict__ x, const T* __restrict__ w,
                                               const T* __restrict__ b, T* __restrict__ y, float* mean_out,
-                                              float* rstd_out, long rows, int C, float eps) {
+                                              float* rstd_out, long rows, int C, float eps, const T* __restrict__ res,
+                                              const dfk_drop drop) {
   constexpr int RPW = 64 / L;  // rows per wave
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane % L;
@@ -80,6 +81,8 @@ __global__ __launch_bounds__(256) void ln_fwd(const T* __restrict__ x, const T* 
     for (int e = 0; e < 8; ++e) { const float d = ok ? v[i][e] - mean : 0.f; q += d * d; }
   }
   const float rstd = rsqrtf(group_sum<L>(q) / C + eps);
+  const DropCtx dc = drop_ctx(drop);
+  const float gmul = dc.mode == 2 ? drop_mul(dc, row, 0) : 1.f;
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int vi = li + i * L;
@@ -89,6 +92,19 @@ __global__ __launch_bounds__(256) void ln_fwd(const T* __restrict__ x, const T* 
     load8m<T>(b, vi * 8, ok, bv);
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * wv[e] + bv[e];
+    if (dc.mode == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] *= gmul;
+    } else if (dc.mode == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] *= drop_mul(dc, row, vi * 8 + e);
+    }
+    if (res) {
+      float rv[8];
+      load8m<T>(res, roff + vi * 8, rok && ok, rv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += rv[e];
+    }
     if (rok && ok) store8<T>(y + row * C + vi * 8, o);
   }
   if (rok && li == 0) {
@@ -102,7 +118,8 @@ template <typename T, int L, int V>
 __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T* __restrict__ x,
                                               const T* __restrict__ w, const float* __restrict__ mean,
                                               const float* __restrict__ rstd, T* __restrict__ dx, float* dw,
-                                              float* db, long rows, int C, int accumulate, float* __restrict__ part) {
+                                              float* db, long rows, int C, int accumulate, float* __restrict__ part,
+                                              const dfk_drop drop) {
   constexpr int RPW = 64 / L;
   constexpr bool KEEP = V <= 4;   // x, dy stay in registers between the two sweeps
   extern __shared__ float red[];  // [2][C] block partials of dw, db
@@ -119,12 +136,23 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
 #pragma unroll
     for (int e = 0; e < 8; ++e) { pw[i][e] = 0.f; pb[i][e] = 0.f; }
   __syncthreads();
+  const DropCtx dc = drop_ctx(drop);   // the forward's mask on dy (gradient of drop(LN(x)))
   const long step = (long)gridDim.x * 4 * RPW;
   for (long r0 = ((long)blockIdx.x * 4 + wave) * RPW; r0 < rows; r0 += step) {
     const long row = r0 + lane / L;
     const bool rok = row < rows;
     const long roff = rok ? row * C : 0;
     const float mu = mean[rok ? row : 0], rs = rstd[rok ? row : 0];
+    const float gmul = dc.mode == 2 ? drop_mul(dc, row, 0) : 1.f;
+    auto dmask = [&](float (&dv)[8], int vi) {
+      if (dc.mode == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dv[e] *= gmul;
+      } else if (dc.mode == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dv[e] *= drop_mul(dc, row, vi * 8 + e);
+      }
+    };
     float xs[KEEP ? V : 1][8], ds[KEEP ? V : 1][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -134,6 +162,7 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
       float xv[8], dv[8];
       load8m<T>(x, roff + vi * 8, ok, xv);
       load8m<T>(dy, roff + vi * 8, ok, dv);
+      dmask(dv, vi);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xh = (xv[e] - mu) * rs, g = dv[e] * wv[i][e];
@@ -156,6 +185,7 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
       } else {
         load8m<T>(x, roff + vi * 8, ok, xv);
         load8m<T>(dy, roff + vi * 8, ok, dv);
+        dmask(dv, vi);
       }
       if (accumulate) load8m<T>(dx, roff + vi * 8, ok, o);
 #pragma unroll
@@ -221,19 +251,19 @@ long bwd_blocks(long rows, int C) {
 
 template <typename T, int L, int V>
 void fwd_launch(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, long rows, int C,
-                float eps, hipStream_t s) {
+                float eps, const void* res, dfk_drop drop, hipStream_t s) {
   const long per_block = 4L * (64 / L);
   hipLaunchKernelGGL((ln_fwd<T, L, V>), dim3((unsigned)dfk_cdiv(rows, per_block)), dim3(256), 0, s, (const T*)x,
-                     (const T*)w, (const T*)b, (T*)y, mean, rstd, rows, C, eps);
+                     (const T*)w, (const T*)b, (T*)y, mean, rstd, rows, C, eps, (const T*)res, drop);
 }
 
 template <typename T, int L, int V>
 void bwd_launch(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx, float* dw,
-                float* db, long rows, int C, int accumulate, float* ws, hipStream_t s) {
+                float* db, long rows, int C, int accumulate, float* ws, dfk_drop drop, hipStream_t s) {
   const int blocks = (int)bwd_blocks(rows, C);
   float* part = ws && (dw || db) ? ws : nullptr;
   hipLaunchKernelGGL((ln_bwd<T, L, V>), dim3(blocks), dim3(256), 2 * C * sizeof(float), s, (const T*)dy,
-                     (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part);
+                     (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part, drop);
   if (part) {
     const dim3 g(dfk_cdiv(C, 256), dfk_cdiv(blocks, 64));
     hipLaunchKernelGGL(slab_colsum, g, dim3(256), 0, s, part, blocks, 2 * C, 0, C, dw);
@@ -263,27 +293,37 @@ bool pick(int C, Args... args) {
 template <typename T, int L, int V>
 struct Fwd {
   static void run(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, long rows, int C,
-                  float eps, hipStream_t s) {
-    fwd_launch<T, L, V>(x, w, b, y, mean, rstd, rows, C, eps, s);
+                  float eps, const void* res, dfk_drop drop, hipStream_t s) {
+    fwd_launch<T, L, V>(x, w, b, y, mean, rstd, rows, C, eps, res, drop, s);
   }
 };
 
 template <typename T, int L, int V>
 struct Bwd {
   static void run(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
-                  float* dw, float* db, long rows, int C, int accumulate, float* ws, hipStream_t s) {
-    bwd_launch<T, L, V>(dy, x, w, mean, rstd, dx, dw, db, rows, C, accumulate, ws, s);
+                  float* dw, float* db, long rows, int C, int accumulate, float* ws, dfk_drop drop, hipStream_t s) {
+    bwd_launch<T, L, V>(dy, x, w, mean, rstd, dx, dw, db, rows, C, accumulate, ws, drop, s);
   }
 };
+
+dfk_drop drop_or_none(const dfk_drop* d) {
+  dfk_drop z = {nullptr, 0, 0, 0.f, 1, 0};
+  return d && d->rng && d->mode ? *d : z;
+}
+
+bool drop_ok(const dfk_drop* d) { return !d || !d->mode || (d->rng && d->p >= 0.f && d->p < 1.f); }
 
 }  // namespace
 
 extern "C" int dfk_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
-                                 int64_t rows, int32_t C, float eps, int dtype, hipStream_t s) {
-  if (!x || !w || !b || !y || C <= 0 || C % 8 || C > 4096) return DFK_EINVAL;
+                                 int64_t rows, int32_t C, float eps, int dtype, const void* residual,
+                                 const dfk_drop* drop, hipStream_t s) {
+  if (!x || !w || !b || !y || C <= 0 || C % 8 || C > 4096 || !drop_ok(drop)) return DFK_EINVAL;
   if (rows <= 0) return 0;
-  const bool ok = dtype == DFK_BF16 ? pick<bf16raw, Fwd>(C, x, w, b, y, mean, rstd, (long)rows, (int)C, eps, s)
-                                    : pick<float, Fwd>(C, x, w, b, y, mean, rstd, (long)rows, (int)C, eps, s);
+  const dfk_drop d = drop_or_none(drop);
+  const bool ok = dtype == DFK_BF16
+                      ? pick<bf16raw, Fwd>(C, x, w, b, y, mean, rstd, (long)rows, (int)C, eps, residual, d, s)
+                      : pick<float, Fwd>(C, x, w, b, y, mean, rstd, (long)rows, (int)C, eps, residual, d, s);
   if (!ok) return DFK_EINVAL;
   DFK_CHECK_LAUNCH();
   return 0;
@@ -296,12 +336,13 @@ extern "C" int64_t dfk_layernorm_bwd_workspace(int64_t rows, int32_t C) {
 
 extern "C" int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                                  void* dx, float* dw, float* db, int64_t rows, int32_t C, int accumulate, int dtype,
-                                 float* ws, hipStream_t s) {
-  if (!dy || !x || !w || !mean || !rstd || !dx || C <= 0 || C % 8 || C > 4096) return DFK_EINVAL;
+                                 float* ws, const dfk_drop* drop, hipStream_t s) {
+  if (!dy || !x || !w || !mean || !rstd || !dx || C <= 0 || C % 8 || C > 4096 || !drop_ok(drop)) return DFK_EINVAL;
   if (rows <= 0) return 0;
+  const dfk_drop d = drop_or_none(drop);
   const bool ok = dtype == DFK_BF16
-                      ? pick<bf16raw, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, ws, s)
-                      : pick<float, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, ws, s);
+                      ? pick<bf16raw, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, ws, d, s)
+                      : pick<float, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, ws, d, s);
   if (!ok) return DFK_EINVAL;
   DFK_CHECK_LAUNCH();
   return 0;

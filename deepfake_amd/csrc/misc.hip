@@ -134,9 +134,10 @@ __global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, long n
 //   g = grad + wd*p ; buf = first ? g : mom*buf + g ; p -= lr*buf ; shadow = bf16(p)
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ grad, float* __restrict__ buf,
                            bf16raw* __restrict__ shadow, long n, const float* __restrict__ lr_dev, float lr_host,
-                           float mom, float wd, int first) {
+                           float mom, float wd, int first, const float* __restrict__ gate) {
   const long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i0 >= n) return;
+  if (gate && *gate == 0.f) return;   // LayerDrop-skipped layer: torch's SGD skips grad=None parameters
   const float lr = lr_dev ? *lr_dev : lr_host;
   if (i0 + 4 <= n) {
     float4 pv = *reinterpret_cast<float4*>(p + i0);
@@ -396,7 +397,7 @@ extern "C" int dfk_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_
 
 extern "C" int dfk_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow, int64_t n,
                             const float* lr_dev, float lr, float momentum, float weight_decay, int first_step,
-                            hipStream_t s) {
+                            const float* gate, hipStream_t s) {
   if (!param || !grad || !momentum_buf) return DFK_EINVAL;
   if ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
        reinterpret_cast<uintptr_t>(momentum_buf)) & 15)
@@ -404,7 +405,7 @@ extern "C" int dfk_sgd_step(float* param, const float* grad, float* momentum_buf
   if (n <= 0) return 0;
   const long threads = (n + 3) / 4;
   hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, param, grad, momentum_buf,
-                     (bf16raw*)bf16_shadow, (long)n, lr_dev, lr, momentum, weight_decay, first_step);
+                     (bf16raw*)bf16_shadow, (long)n, lr_dev, lr, momentum, weight_decay, first_step, gate);
   DFK_CHECK_LAUNCH();
   return 0;
 }

@@ -684,7 +684,7 @@ __device__ __forceinline__ float grp_max4(float v) {
 // table (the fp32 table tile is loaded straight into the accumulators, two key blocks ahead), running
 // max in raw units, P = 2^(S*scale*log2e - m) by one fma + exp per score, lazy rescale,
 // O^T += V^T P^T, l = ones^T P^T (the denominator on the MFMA too).
-template <int HD>
+template <int HD, bool DROP = false>
 __global__ __launch_bounds__(256) void wattn_fwd_tab_kernel(const dfk_wattn_args a, const Geo g, int qsplit,
                                                             const float* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -708,6 +708,7 @@ __global__ __launch_bounds__(256) void wattn_fwd_tab_kernel(const dfk_wattn_args
   __syncthreads();
 
   const float scale2 = a.scale * kLog2e;
+  const DropCtx dc = drop_ctx(a.drop);   // DROP: attention-probability dropout (row = unit*Np + q, col = k)
   bf16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
@@ -805,12 +806,26 @@ __global__ __launch_bounds__(256) void wattn_fwd_tab_kernel(const dfk_wattn_args
           for (int r = 0; r < 4; ++r)
             pf[qh][h2 * 4 + r] = (__bf16)__builtin_amdgcn_exp2f(__builtin_fmaf(s[qh][h2][r], scale2, -m2[qh]));
       load_tab(s, min(kb + 2, nkb - 1));   // unconditional (clamped): static vmcnt counts, no phi copies
+      // DROP: O accumulates the dropped probabilities, the denominator l the undropped ones
+      bf16x8 pv[2] = {pf[0], pf[1]};
+      if constexpr (DROP) {
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const long qrow_id = unit * g.Np + qb * 32 + qh * 16 + ql;
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              pv[qh][h2 * 4 + r] = (__bf16)((float)pf[qh][h2 * 4 + r] *
+                                            drop_mul(dc, qrow_id, kb * 32 + h2 * 16 + grp * 4 + r));
+        }
+      }
 #pragma unroll
       for (int et = 0; et < HD / 16; ++et) {
         const int c = et * 16 + tp * 4;
         const bf16x8 va = tr16x2(Vs + swz<HD>(kb * 32 + grp * 4 + tq, c), Vs + swz<HD>(kb * 32 + 16 + grp * 4 + tq, c));
 #pragma unroll
-        for (int qh = 0; qh < 2; ++qh) o[qh][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pf[qh], o[qh][et], 0, 0, 0);
+        for (int qh = 0; qh < 2; ++qh) o[qh][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pv[qh], o[qh][et], 0, 0, 0);
       }
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qh], lsum[qh], 0, 0, 0);
@@ -910,6 +925,7 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
   if (!ap || !args_ok(*ap)) return DFK_EINVAL;
   const dfk_wattn_args& a = *ap;
   const Geo g = make_geo(a);
+  if (a.drop.mode && !(a.dtype == DFK_BF16 && a.tab && !a.mask && a.scale > 0.f)) return DFK_EINVAL;  // table path only
   if (a.dtype == DFK_BF16 && a.tab && !a.mask && a.scale > 0.f) {   // table built by dfk_wattn_table
     const long units = (long)a.B * g.nW * a.heads;
     if (units <= 0) return 0;
@@ -919,9 +935,9 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     const int nw = std::min(4, nqb);
     const int qsplit = (int)std::max<long>(1, std::min<long>(dfk_cdiv(nqb, nw), dfk_cdiv(1024, units)));
     dim3 grid((unsigned)(units * qsplit));
-#define LAUNCH_T(HD)                                                                                         \
+#define LAUNCH_T(HD, DR)                                                                                     \
   do {                                                                                                       \
-    auto kfn = wattn_fwd_tab_kernel<HD>;                                                                     \
+    auto kfn = wattn_fwd_tab_kernel<HD, DR>;                                                                 \
     static bool attr_set = false;                                                                            \
     if (!attr_set) {                                                                                         \
       (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);   \
@@ -929,7 +945,9 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     }                                                                                                        \
     hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), lds, s, a, g, qsplit, (const float*)tf);                 \
   } while (0)
-    if (a.hd == 32) LAUNCH_T(32); else LAUNCH_T(64);
+    const bool dr = a.drop.mode != 0;
+    if (a.hd == 32) { if (dr) LAUNCH_T(32, true); else LAUNCH_T(32, false); }
+    else { if (dr) LAUNCH_T(64, true); else LAUNCH_T(64, false); }
 #undef LAUNCH_T
     DFK_CHECK_LAUNCH();
     return 0;
@@ -1308,7 +1326,7 @@ __global__ __launch_bounds__(256) void wattn_bwd_kernel(const dfk_wattn_bwd_args
 
 // TAB: the score bias (RPB + shift mask, -inf beyond N) comes from the forward's bwd-layout table as the
 // C input of S = Q K^T (no per-score gather, label compare or key mask).
-template <int HD, bool RPB, bool MASK, bool TAB = false>
+template <int HD, bool RPB, bool MASK, bool TAB = false, bool DROP = false>
 __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(const dfk_wattn_bwd_args ba, const Geo g,
                                                                               int q0, int Qn, int accum_kv,
                                                                               bf16raw* __restrict__ dsg,
@@ -1389,6 +1407,7 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
   float* myQ = dQp + wave * 32 * kDqStride;
   const float scale2 = a.scale * kLog2e;
   const float mpen = -100.f * kLog2e;
+  const DropCtx dc = drop_ctx(a.drop);   // DROP: the forward's attention-dropout mask (row = unit*Np + q, col = k)
   bf16raw* dsu = RPB && dsg ? dsg + (long)blockIdx.x * g.Np * g.Np : nullptr;   // this window-head's dS^T [k][q]
   for (int pass = 0; pass * nwaves < nkb; ++pass) {
     const int kb = pass * nwaves + wave;
@@ -1497,8 +1516,12 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
                 if (q < g.N && k < g.N) x += mrow[q * g.N + k] * kLog2e;
               }
               const float P = __builtin_amdgcn_exp2f(x);
-              const float dS = P * (dp[qh][h2][r] - DL[qh][r]);
-              pa[h2][qh * 4 + r] = (__bf16)P;
+              float mk = 1.f;
+              if constexpr (DROP)
+                mk = drop_mul(dc, (long)blockIdx.x * g.Np + q0 + qr0 + qh * 16 + grp * 4 + r, kb * 32 + h2 * 16 + ql);
+              // dropout: dV = (P.Z/keep)^T dO, dS = P (dP.Z/keep - rowsum(dO.O)) with O the dropped output
+              const float dS = P * (dp[qh][h2][r] * mk - DL[qh][r]);
+              pa[h2][qh * 4 + r] = (__bf16)(P * mk);
               sa[h2][qh * 4 + r] = (__bf16)dS;
               dsv[r] = dS;
             }
@@ -1695,11 +1718,15 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
 #define LAUNCH_B16(HD, RPB, MASK)                                                                          \
   do {                                                                                                     \
     auto kfn = wattn_bwd_bf16_kernel<HD, RPB, MASK>;                                                       \
-    auto kft = wattn_bwd_bf16_kernel<HD, RPB, false, true>;                                                \
+    auto kft = a.drop.mode ? wattn_bwd_bf16_kernel<HD, RPB, false, true, true>                           \
+                           : wattn_bwd_bf16_kernel<HD, RPB, false, true, false>;                          \
     static bool attr_set = false;                                                                          \
     if (!attr_set) {                                                                                       \
       (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
-      (void)hipFuncSetAttribute((const void*)kft, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      (void)hipFuncSetAttribute((const void*)wattn_bwd_bf16_kernel<HD, RPB, false, true, false>,           \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                   \
+      (void)hipFuncSetAttribute((const void*)wattn_bwd_bf16_kernel<HD, RPB, false, true, true>,            \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                   \
       attr_set = true;                                                                                     \
     }                                                                                                      \
     for (int q0 = 0; q0 < g.Np; q0 += Qn)                                                                  \
@@ -1718,6 +1745,7 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     // the forward left both table layouts in a.tab (same args, same rpb): the bwd layout follows the fwd one
     const float* tabb = a.tab && !a.mask && a.scale > 0.f ? reinterpret_cast<const float*>(a.tab) + tab_elems(a, g)
                                                           : nullptr;
+    if (a.drop.mode && !tabb) return DFK_EINVAL;   // attention dropout: table path only (as the forward)
     if (a.hd == 32) PICK_B16(32); else PICK_B16(64);
 #undef PICK_B16
 #undef LAUNCH_B16
@@ -1733,6 +1761,7 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     return 0;
   }
   // fp32 (parity mode): largest query chunk (multiple of 32) that fits the 160 KiB LDS
+  if (a.drop.mode) return DFK_EINVAL;
   int Qn = g.Np;
   while (Qn > 32 && bwd_lds(a, g, Qn) > 160 * 1024) Qn -= 32;
   const size_t lds = bwd_lds(a, g, Qn);

@@ -81,6 +81,7 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   bf16raw* aux = reinterpret_cast<bf16raw*>(g.aux);
   bf16raw* C = reinterpret_cast<bf16raw*>(g.c);
   const int mrow = lane & 15, kq = (lane >> 4) * 8, nq = (lane >> 4) * 4;
+  const DropCtx dc = drop_ctx(g.drop);   // dropout / DropPath of the output (mode 0: none)
   const bf16raw* wbase = w_lds + (cg * NBW * 16 + mrow) * WS + kq;
 
   // this wave's fragment row of tile t: token m = t*ROWS_T + rg*16 + (lane&15)
@@ -163,6 +164,7 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
       if (staged) flush(aux, g.ldaux);
     }
     {
+      const float gmul = dc.mode == 2 ? drop_mul(dc, m, 0) : 1.f;   // DropPath: one draw per token group
 #pragma unroll
       for (int nb = 0; nb < NBW; ++nb) {
         const int n = c0 + nb * 16 + nq;
@@ -180,6 +182,13 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
           const uint2 a = *reinterpret_cast<const uint2*>(aux + m * g.ldaux + n);
           v[0] *= dgelu_f(__uint_as_float(a.x << 16)); v[1] *= dgelu_f(__uint_as_float(a.x & 0xffff0000u));
           v[2] *= dgelu_f(__uint_as_float(a.y << 16)); v[3] *= dgelu_f(__uint_as_float(a.y & 0xffff0000u));
+        }
+        if (dc.mode == 2) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= gmul;
+        } else if (dc.mode == 1) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= drop_mul(dc, m, n + e);
         }
         if (res && ok) {
           const uint2 r = *reinterpret_cast<const uint2*>(res + m * g.ldr + n);

@@ -66,26 +66,28 @@ def rows2d(x):
 
 
 class LinearFn(torch.autograd.Function):
-    """y = x W^T + b (act 1: y = gelu(.)) (+ residual).  nn.Linear / F.linear."""
+    """y = drop(x W^T + b) (act 1: drop(gelu(.))) (+ residual).  nn.Linear / F.linear, with the
+    dropout / DropPath that follows it in the reference (rng.Drop spec, applied before the residual add)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, act, residual):
+    def forward(ctx, x, weight, bias, act, residual, drop=None):
         dt = x.dtype
         w = compute_weight(weight, dt)
         b = compute_weight(bias, dt)
         aux = torch.empty(x.shape[0], weight.shape[0], device=x.device, dtype=dt) if act == 1 else None
-        y = K.linear(x, w, b, act=act, aux=aux, residual=residual)
+        y = K.linear(x, w, b, act=act, aux=aux, residual=residual, drop=drop)
         grad_use(ctx, 1, weight)
         grad_use(ctx, 2, bias)
         ctx.save_for_backward(x, weight, bias, aux)
-        ctx.act, ctx.has_bias, ctx.has_res = act, bias is not None, residual is not None
+        ctx.act, ctx.has_bias, ctx.has_res, ctx.drop = act, bias is not None, residual is not None, drop
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, weight, bias, aux = ctx.saved_tensors
         dy = dy.contiguous()
-        dz = K.gelu_bwd(dy, aux) if ctx.act == 1 else dy
+        dz = K.dropout(dy, ctx.drop) if ctx.drop is not None else dy
+        dz = K.gelu_bwd(dz, aux) if ctx.act == 1 else dz
         w = compute_weight(weight, x.dtype)
         dx = K.linear_dx(dz, w) if ctx.needs_input_grad[0] else None
         dw = db = None
@@ -97,39 +99,43 @@ class LinearFn(torch.autograd.Function):
             db = K.colsum(dz, grad_sink(bias))
         if want_b:
             db = grad_done(bias, db)
-        return dx, dw, db, None, (dy if ctx.has_res else None)
+        return dx, dw, db, None, (dy if ctx.has_res else None), None
 
 
-def linear(x, weight, bias=None, act=0, residual=None):
+def linear(x, weight, bias=None, act=0, residual=None, drop=None):
     shp = x.shape
     y = LinearFn.apply(rows2d(x).contiguous(), weight, bias, act,
-                       rows2d(residual).contiguous() if residual is not None else None)
+                       rows2d(residual).contiguous() if residual is not None else None, drop)
     return y.view(*shp[:-1], weight.shape[0])
 
 
 class MlpFn(torch.autograd.Function):
-    """residual + fc2(gelu(fc1(x))) — src/utils.py:242-260 Mlp (dropout 0) fused
-    with the block residual (video_swin_transformer.py:276)."""
+    """residual + drop_out(fc2(drop_act(gelu(fc1(x))))) — src/utils.py:242-260 Mlp / HF Wav2Vec2FeedForward
+    (:551-573: activation dropout after the GELU, hidden dropout after fc2) fused with the block residual
+    (video_swin_transformer.py:276: DropPath of the branch = drop_out in group mode)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, residual):
+    def forward(ctx, x, w1, b1, w2, b2, residual, drop_act=None, drop_out=None):
         dt = x.dtype
         W1, B1, W2, B2 = (compute_weight(t, dt) for t in (w1, b1, w2, b2))
         pre = torch.empty(x.shape[0], w1.shape[0], device=x.device, dtype=dt)
-        h = K.linear(x, W1, B1, act=1, aux=pre)
-        y = K.linear(h, W2, B2, residual=residual)
+        h = K.linear(x, W1, B1, act=1, aux=pre, drop=drop_act)
+        y = K.linear(h, W2, B2, residual=residual, drop=drop_out)
         for i, p in enumerate((w1, b1, w2, b2)):
             grad_use(ctx, 1 + i, p)
         ctx.save_for_backward(x, w1, b1, w2, b2, pre, h)
-        ctx.has_res = residual is not None
+        ctx.has_res, ctx.drop_act, ctx.drop_out = residual is not None, drop_act, drop_out
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w1, b1, w2, b2, pre, h = ctx.saved_tensors
         dy = dy.contiguous()
+        dyr = dy
+        if ctx.drop_out is not None:
+            dy = K.dropout(dy, ctx.drop_out)
         dt = x.dtype
-        dpre = K.linear_dx(dy, compute_weight(w2, dt), act=2, aux=pre)      # (dy W2) * gelu'(pre)
+        dpre = K.linear_dx(dy, compute_weight(w2, dt), act=2, aux=pre, drop=ctx.drop_act)   # (dy W2).Z * gelu'(pre)
         db2 = grad_sink(b2)
         dw2 = grad_done(w2, K.linear_dw(dy, h, grad_sink(w2), db=db2))
         db2 = grad_done(b2, db2)
@@ -137,37 +143,44 @@ class MlpFn(torch.autograd.Function):
         db1 = grad_sink(b1)
         dw1 = grad_done(w1, K.linear_dw(dpre, x, grad_sink(w1), db=db1))
         db1 = grad_done(b1, db1)
-        return dx, dw1, db1, dw2, db2, (dy if ctx.has_res else None)
+        return dx, dw1, db1, dw2, db2, (dyr if ctx.has_res else None), None, None
 
 
-def mlp(x, fc1, fc2, residual=None):
+def mlp(x, fc1, fc2, residual=None, drop_act=None, drop_out=None):
     shp = x.shape
     y = MlpFn.apply(rows2d(x).contiguous(), fc1.weight, fc1.bias, fc2.weight, fc2.bias,
-                    rows2d(residual).contiguous() if residual is not None else None)
+                    rows2d(residual).contiguous() if residual is not None else None, drop_act, drop_out)
     return y.view(*shp[:-1], fc2.weight.shape[0])
 
 
 class LayerNormFn(torch.autograd.Function):
+    """y = LN(x), or residual + drop(LN(x)) (SwinV2 post-norm x + DropPath(LN(a)), swin_transformer2d.py:301,304;
+    wav2vec2 LN -> dropout, HF :691-692)."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias, eps):
+    def forward(ctx, x, weight, bias, eps, residual=None, drop=None):
         dt = x.dtype
-        y, mean, rstd = K.layernorm_fwd(x, compute_weight(weight, dt), compute_weight(bias, dt), eps)
+        y, mean, rstd = K.layernorm_fwd(x, compute_weight(weight, dt), compute_weight(bias, dt), eps,
+                                        residual=residual, drop=drop)
         grad_use(ctx, 1, weight)
         grad_use(ctx, 2, bias)
         ctx.save_for_backward(x, weight, bias, mean, rstd)
+        ctx.drop, ctx.has_res = drop, residual is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, weight, bias, mean, rstd = ctx.saved_tensors
+        dy = dy.contiguous()
         dw, db = grad_sink(weight), grad_sink(bias)
-        dx = K.layernorm_bwd(dy.contiguous(), x, compute_weight(weight, x.dtype), mean, rstd, dw, db)
-        return dx, grad_done(weight, dw), grad_done(bias, db), None
+        dx = K.layernorm_bwd(dy, x, compute_weight(weight, x.dtype), mean, rstd, dw, db, drop=ctx.drop)
+        return dx, grad_done(weight, dw), grad_done(bias, db), None, (dy if ctx.has_res else None), None
 
 
-def layer_norm(x, ln):
+def layer_norm(x, ln, residual=None, drop=None):
     shp = x.shape
-    return LayerNormFn.apply(rows2d(x).contiguous(), ln.weight, ln.bias, ln.eps).view(shp)
+    return LayerNormFn.apply(rows2d(x).contiguous(), ln.weight, ln.bias, ln.eps,
+                             rows2d(residual).contiguous() if residual is not None else None, drop).view(shp)
 
 
 class WindowAttnFn(torch.autograd.Function):
@@ -177,7 +190,7 @@ class WindowAttnFn(torch.autograd.Function):
     [3C] (the padded positions' q/k/v, or None), explicit mask or None."""
 
     @staticmethod
-    def forward(ctx, qkv, rpb, qkv_bias, mask, geo):
+    def forward(ctx, qkv, rpb, qkv_bias, mask, geo, drop=None):
         dims, window, full_window, shift, heads, hd, scale = geo
         C = heads * hd
         pads = None
@@ -186,12 +199,12 @@ class WindowAttnFn(torch.autograd.Function):
             pads = (bc[:C], bc[C:2 * C], bc[2 * C:])
         rpb_f = rpb.detach().float().contiguous() if rpb is not None else None
         out, lse, tab = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], qkv.stride(0), dims, window, full_window, shift,
-                                    heads, hd, scale, rpb=rpb_f, pads=pads, mask=mask, return_table=True)
+                                    heads, hd, scale, rpb=rpb_f, pads=pads, mask=mask, return_table=True, drop=drop)
         ctx.tab = tab
         grad_use(ctx, 1, rpb)
         grad_use(ctx, 2, qkv_bias)
         ctx.save_for_backward(qkv, out, lse, rpb_f, mask, rpb, qkv_bias)
-        ctx.pads, ctx.geo = pads, geo
+        ctx.pads, ctx.geo, ctx.drop = pads, geo, drop
         ctx.has_rpb, ctx.has_bias = rpb is not None, qkv_bias is not None
         return out
 
@@ -208,17 +221,52 @@ class WindowAttnFn(torch.autograd.Function):
         dpads = [dbias[i * C:(i + 1) * C] for i in range(3)] if ctx.has_bias else None
         K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, qkv.stride(0), dims, window, full_window, shift, heads,
                      hd, scale, rpb_f, ctx.pads), dout.contiguous(), dqkv, dqkv[:, C:], dqkv[:, 2 * C:], qkv.stride(0),
-                    drpb=drpb, dpads=dpads, mask=mask, tab=ctx.tab)
+                    drpb=drpb, dpads=dpads, mask=mask, tab=ctx.tab, drop=ctx.drop)
         ctx.tab = None
         if ctx.has_rpb:
             drpb = grad_done(rpb, drpb)
         if ctx.has_bias:
             dbias = grad_done(qkv_bias, dbias)
-        return dqkv, drpb, dbias, None, None
+        return dqkv, drpb, dbias, None, None, None
 
 
-def window_attention(qkv, rpb, qkv_bias, geo, mask=None):
-    return WindowAttnFn.apply(qkv, rpb, qkv_bias, mask, geo)
+def window_attention(qkv, rpb, qkv_bias, geo, mask=None, drop=None):
+    """drop: attention-probability dropout (bf16 table path only)."""
+    if drop is not None and qkv.dtype != torch.bfloat16:
+        raise NotImplementedError("attention dropout runs in the bf16 table kernels only (fp32 parity mode: p = 0)")
+    return WindowAttnFn.apply(qkv, rpb, qkv_bias, mask, geo, drop)
+
+
+class DropoutFn(torch.autograd.Function):
+    """nn.Dropout / DropPath as a standalone pass on a 2-D view: y = x * mask / (1 - p)."""
+
+    @staticmethod
+    def forward(ctx, x, drop):
+        ctx.drop = drop
+        return K.dropout(x, drop)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K.dropout(dy.contiguous(), ctx.drop), None
+
+
+class SpecAugmentFn(torch.autograd.Function):
+    """HF Wav2Vec2Model._mask_hidden_states time masking (:1272-1317): masked frames <- masked_spec_embed."""
+
+    @staticmethod
+    def forward(ctx, h, embed, mask_prob, mask_length, min_masks, drop):
+        e = compute_weight(embed, h.dtype).contiguous()
+        out, mask = K.spec_augment_fwd(h.contiguous(), e, mask_prob, mask_length, min_masks, drop)
+        grad_use(ctx, 1, embed)
+        ctx.save_for_backward(mask, embed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        mask, embed = ctx.saved_tensors
+        de = grad_sink(embed)
+        dx = K.spec_augment_bwd(dy.contiguous(), mask, de)
+        return dx, grad_done(embed, de), None, None, None, None
 
 
 class PatchMergeFn(torch.autograd.Function):

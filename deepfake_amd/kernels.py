@@ -26,9 +26,12 @@ def _view(t, ld, bs0=0, bs1=0, conv=None):
 def gemm(a, a_ld, a_kmajor, b, b_ld, b_kmajor, M, N, K, c, ldc, *, dtype, c_f32=False, bias=None,
          residual=None, ldr=0, aux=None, ldaux=0, act=0, beta=0.0, atomic=False, splitk=1,
          nz=(1, 1), a_bs=(0, 0), b_bs=(0, 0), c_bs=(0, 0), r_bs=(0, 0), a_conv=None, b_conv=None, bias_bs1=0,
-         rowsum=None):
-    """Raw dfk_gemm.  a/b/c are tensors (base pointers); see include/dfk.h."""
+         rowsum=None, drop=None):
+    """Raw dfk_gemm.  a/b/c are tensors (base pointers); see include/dfk.h.  drop: rng.Drop spec of the
+    output's dropout / DropPath (applied before the residual add)."""
     g = L.GemmArgs()
+    if drop is not None:
+        g.drop = L.drop(drop, c.device)
     g.bias_bs1 = int(bias_bs1)
     g.a = _view(a, a_ld, *a_bs, conv=a_conv)
     g.b = _view(b, b_ld, *b_bs, conv=b_conv)
@@ -60,26 +63,26 @@ def gemm(a, a_ld, a_kmajor, b, b_ld, b_kmajor, M, N, K, c, ldc, *, dtype, c_f32=
     L.check(L.lib().dfk_gemm(g, L.stream()), f"gemm M={M} N={N} K={K}")
 
 
-def linear(x, w, b=None, act=0, aux=None, residual=None, out=None, beta=0.0):
-    """y[M,N] = x[M,K] @ w[N,K]^T (+b) (gelu: act=1, preact -> aux) (+residual)."""
+def linear(x, w, b=None, act=0, aux=None, residual=None, out=None, beta=0.0, drop=None):
+    """y[M,N] = x[M,K] @ w[N,K]^T (+b) (gelu: act=1, preact -> aux) (dropout) (+residual)."""
     M, K = x.shape
     N = w.shape[0]
     if out is None:
         out = torch.empty(M, N, device=x.device, dtype=x.dtype)
     gemm(x, x.stride(0), False, w, w.stride(0), False, M, N, K, out, out.stride(0), dtype=L.dt(x), bias=b,
          residual=residual, ldr=residual.stride(0) if residual is not None else 0, aux=aux,
-         ldaux=aux.stride(0) if aux is not None else 0, act=act, beta=beta)
+         ldaux=aux.stride(0) if aux is not None else 0, act=act, beta=beta, drop=drop)
     return out
 
 
-def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0):
-    """dx[M,K] = dy[M,N] @ w[N,K]  (act=2: times gelu'(aux))."""
+def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None):
+    """dx[M,K] = dy[M,N] @ w[N,K]  (act=2: times gelu'(aux)) (drop: times the forward's dropout mask)."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dy.device, dtype=dy.dtype)
     gemm(dy, dy.stride(0), False, w, w.stride(0), True, M, K, N, out, out.stride(0), dtype=L.dt(dy), act=act,
-         aux=aux, ldaux=aux.stride(0) if aux is not None else 0, beta=beta)
+         aux=aux, ldaux=aux.stride(0) if aux is not None else 0, beta=beta, drop=drop)
     return out
 
 
@@ -110,18 +113,20 @@ def colsum(x, out):
     return out
 
 
-def layernorm_fwd(x, w, b, eps=1e-5, out=None):
+def layernorm_fwd(x, w, b, eps=1e-5, out=None, residual=None, drop=None):
+    """y = LN(x) (residual + drop(LN(x)) with residual / drop)."""
     rows, C = x.shape
     if out is None:
         out = torch.empty_like(x)
     mean = torch.empty(rows, device=x.device, dtype=torch.float32)
     rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    d = L.drop(drop, x.device)
     L.check(L.lib().dfk_layernorm_fwd(L.ptr(x), L.ptr(w), L.ptr(b), L.ptr(out), L.ptr(mean), L.ptr(rstd), rows, C,
-                                      float(eps), L.dt(x), L.stream()), "layernorm_fwd")
+                                      float(eps), L.dt(x), L.ptr(residual), d, L.stream()), "layernorm_fwd")
     return out, mean, rstd
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False, slab_partials=False):
+def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False, slab_partials=False, drop=None):
     rows, C = x.shape
     if dx is None:
         dx = torch.empty_like(x)
@@ -131,13 +136,15 @@ def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False, slab_
                          dtype=torch.float32)
     L.check(L.lib().dfk_layernorm_bwd(L.ptr(dy), L.ptr(x), L.ptr(w), L.ptr(mean), L.ptr(rstd), L.ptr(dx),
                                       L.ptr(dw), L.ptr(db), rows, C, int(accumulate), L.dt(x), L.ptr(ws),
-                                      L.stream()), "layernorm_bwd")
+                                      L.drop(drop, x.device), L.stream()), "layernorm_bwd")
     return dx
 
 
 def wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb=None, pads=None,
-               lse=None, mask=None):
+               lse=None, mask=None, drop=None):
     a = L.WattnArgs()
+    if drop is not None:
+        a.drop = L.drop(drop, q.device)
     if mask is not None:
         a.mask, a.mask_nw = mask.data_ptr(), int(mask.shape[0])
     a.q, a.k, a.v, a.out = q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
@@ -166,7 +173,7 @@ def window_geometry(dims, window):
 
 
 def wattn_fwd(q, k, v, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb=None, pads=None,
-              out=None, need_lse=True, mask=None, use_table=True, return_table=False, tab=None):
+              out=None, need_lse=True, mask=None, use_table=True, return_table=False, tab=None, drop=None):
     """Token-major window attention core; returns (out [rows, heads*hd], lse[, tab]).
     use_table: bf16 score-bias tables (RPB + shift mask per shift class, built by dfk_wattn_table, or
     `tab` from an earlier call with the same geometry and rpb); the backward must get the same `tab`."""
@@ -175,7 +182,8 @@ def wattn_fwd(q, k, v, ld_qkv, dims, window, full_window, shift, heads, hd, scal
         out = torch.empty(rows, heads * hd, device=q.device, dtype=q.dtype)
     nW, N, Np = window_geometry(dims, window)
     lse = torch.empty(dims[0] * nW * heads, Np, device=q.device, dtype=torch.float32) if need_lse else None
-    a = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse, mask)
+    a = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse, mask,
+                   drop)
     if tab is not None:
         a.tab = tab.data_ptr()
     elif use_table and os.environ.get("DFK_WATTN_TABLE", "1") != "0":
@@ -192,12 +200,13 @@ def wattn_fwd(q, k, v, ld_qkv, dims, window, full_window, shift, heads, hd, scal
     return out, lse
 
 
-def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None, mask=None, tab=None):
+def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None, mask=None, tab=None, drop=None):
     """Backward of wattn_fwd.  fwd_args_tensors = (q, k, v, out, lse, ld_qkv, dims, window, full_window,
     shift, heads, hd, scale, rpb, pads).  dq/dk/dv may alias column slices of one [rows, 3C] buffer."""
     (q, k, v, out, lse, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads) = fwd_args_tensors
     ba = L.WattnBwdArgs()
-    ba.f = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse, mask)
+    ba.f = wattn_args(q, k, v, out, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads, lse, mask,
+                      drop)
     if tab is not None:
         ba.f.tab = tab.data_ptr()
     ba.dout = dout.data_ptr()
@@ -359,7 +368,43 @@ def wave_normalize(wave, eps=1e-7):
     return out
 
 
-def sgd_step(param, grad, buf, shadow, lr, momentum, wd, first, lr_dev=None):
+def sgd_step(param, grad, buf, shadow, lr, momentum, wd, first, lr_dev=None, gate=None):
     L.check(L.lib().dfk_sgd_step(L.ptr(param), L.ptr(grad), L.ptr(buf), L.ptr(shadow) if shadow is not None else None,
                                  param.numel(), L.ptr(lr_dev) if lr_dev is not None else None, float(lr),
-                                 float(momentum), float(wd), int(first), L.stream()), "sgd_step")
+                                 float(momentum), float(wd), int(first), L.ptr(gate), L.stream()), "sgd_step")
+
+
+def dropout(x, drop, out=None, group_rows=None):
+    """out = x * mask / (1 - p) over a 2-D [rows, cols] view (out may be x)."""
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    L.check(L.lib().dfk_dropout(L.ptr(x), L.ptr(out), rows, cols, x.stride(0), L.drop(drop, x.device), L.dt(x),
+                                L.stream()), "dropout")
+    return out
+
+
+def bernoulli_flags(drop, n, device):
+    """fp32 [n] of 1 (keep) / 0 (drop) coins (LayerDrop)."""
+    out = torch.empty(n, device=device, dtype=torch.float32)
+    L.check(L.lib().dfk_bernoulli_flags(L.drop(drop, device), n, L.ptr(out), L.stream()), "bernoulli_flags")
+    return out
+
+
+def spec_augment_fwd(h, embed, mask_prob, mask_length, min_masks, drop):
+    """h [B, T, C] -> (masked copy, mask [B, T] uint8)."""
+    B, T, C = h.shape
+    out = torch.empty_like(h)
+    mask = torch.empty(B, T, device=h.device, dtype=torch.uint8)
+    L.check(L.lib().dfk_spec_augment_fwd(L.ptr(h), L.ptr(out), L.ptr(mask), L.ptr(embed), B, T, C, float(mask_prob),
+                                         int(mask_length), int(min_masks), L.drop(drop, h.device), L.dt(h),
+                                         L.stream()), "spec_augment_fwd")
+    return out, mask
+
+
+def spec_augment_bwd(dy, mask, dembed):
+    B, T, C = dy.shape
+    dx = torch.empty_like(dy)
+    L.check(L.lib().dfk_spec_augment_bwd(L.ptr(dy), L.ptr(dx), L.ptr(mask), L.ptr(dembed), B, T, C, L.dt(dy),
+                                         L.stream()), "spec_augment_bwd")
+    return dx

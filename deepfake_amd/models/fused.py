@@ -53,7 +53,8 @@ def build_fused(cfg, args=None, w2v_config=W2V_CONFIG, compute_dtype=torch.float
     mask_time_prob, Audio2D's dropout (args.swin_drop) and the head's (args.classify_drop)."""
     if isinstance(cfg, str):
         cfg = CONFIGS[cfg]
-    args = args or types.SimpleNamespace(soft=0.01, classify_drop=0.0, swin_drop=0.0)
+    d = 0.1 if regularize else 0.0   # config.py:30-31 defaults of --classify_drop / --swin_drop
+    args = args or types.SimpleNamespace(soft=0.01, classify_drop=d, swin_drop=d)
     vkw, mkw = dict(cfg["vst"]), dict(cfg["mel"])
     if regularize:
         vkw["drop_path_rate"], mkw["drop_path_rate"] = 0.2, 0.1

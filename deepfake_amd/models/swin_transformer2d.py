@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 
 from .. import functional as Fn
+from .. import rng
 
 
 def to_2tuple(x):
@@ -110,8 +111,8 @@ class SwinTransformerBlock(nn.Module):
                  drop=0., attn_drop=0., drop_path=0., act_layer=nn.GELU, norm_layer=nn.LayerNorm,
                  pretrained_window_size=0):
         super().__init__()
-        if drop_path > 0 or drop > 0:
-            raise NotImplementedError("DropPath/dropout > 0 is not implemented on the MI355X path")
+        if drop > 0:
+            raise NotImplementedError("dropout > 0 in the SwinV2 block is not implemented on the MI355X path")
         self.dim, self.input_resolution, self.num_heads = dim, input_resolution, num_heads
         self.window_size, self.shift_size, self.mlp_ratio = window_size, shift_size, mlp_ratio
         if min(self.input_resolution) <= self.window_size:
@@ -123,6 +124,8 @@ class SwinTransformerBlock(nn.Module):
                                     qkv_bias=qkv_bias, attn_drop=attn_drop, proj_drop=drop,
                                     pretrained_window_size=to_2tuple(pretrained_window_size))
         self.drop_path = nn.Identity()
+        # timm DropPath is called once per branch: two independent per-sample draws
+        self.dp = (rng.Drop(drop_path, mode=2), rng.Drop(drop_path, mode=2)) if drop_path > 0 else None
         self.norm2 = norm_layer(dim)
         self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
         if self.shift_size > 0:
@@ -147,9 +150,11 @@ class SwinTransformerBlock(nn.Module):
         x2 = x.reshape(-1, C)
         a = self.attn.core(x2, (B, 1, H, W), self.window_size, self.shift_size)
         a = Fn.linear(a, self.attn.proj.weight, self.attn.proj.bias)
-        x2 = x2 + Fn.layer_norm(a, self.norm1)
+        on = self.dp is not None and self.training
+        dp = (self.dp[0].spec(L), self.dp[1].spec(L)) if on else (None, None)
+        x2 = Fn.layer_norm(a, self.norm1, residual=x2, drop=dp[0])   # x + DropPath(LN(attn)) (:301)
         m = Fn.mlp(x2, self.mlp.fc1, self.mlp.fc2)
-        x2 = x2 + Fn.layer_norm(m, self.norm2)
+        x2 = Fn.layer_norm(m, self.norm2, residual=x2, drop=dp[1])   # x + DropPath(LN(mlp)) (:304)
         return x2.view(B, L, C)
 
 

@@ -11,8 +11,11 @@ BasicLayer/SwinTransformer3D API) are converted only at the public API
 entry/exit; the fused model's video extractor (VSTFeat) never leaves the
 token layout.
 
-Not implemented on the hot path (round 1): stochastic depth (DropPath) and
-dropout with p>0 — construct with drop_path_rate/drop_rate > 0 raises.
+Stochastic depth (timm DropPath, :214) runs in training mode as a per-clip
+mask fused into the proj / fc2 GEMM epilogues (rng.Drop mode 2, one draw per
+clip's tokens, scaled 1/(1-p)); the backward applies the same mask to the
+branch gradient.  Plain dropout / attention dropout with p > 0 (drop_rate,
+attn_drop_rate: 0 in every reference configuration) raise.
 """
 from functools import lru_cache
 
@@ -20,6 +23,7 @@ import torch
 import torch.nn as nn
 
 from .. import functional as Fn
+from .. import rng
 from ..utils import Mlp
 
 
@@ -117,8 +121,8 @@ class SwinTransformerBlock3D(nn.Module):
                  qk_scale=None, drop=0., attn_drop=0., drop_path=0., act_layer=nn.GELU, norm_layer=nn.LayerNorm,
                  use_checkpoint=False):
         super().__init__()
-        if drop_path > 0 or drop > 0:
-            raise NotImplementedError("DropPath/dropout > 0 is not implemented on the MI355X path")
+        if drop > 0:
+            raise NotImplementedError("dropout > 0 in the Swin3D block is not implemented on the MI355X path")
         self.dim, self.num_heads = dim, num_heads
         self.window_size, self.shift_size = tuple(window_size), tuple(shift_size)
         self.mlp_ratio, self.use_checkpoint = mlp_ratio, use_checkpoint
@@ -127,6 +131,8 @@ class SwinTransformerBlock3D(nn.Module):
         self.attn = WindowAttention3D(dim, window_size=self.window_size, num_heads=num_heads, qkv_bias=qkv_bias,
                                       qk_scale=qk_scale, attn_drop=attn_drop, proj_drop=drop)
         self.drop_path = nn.Identity()
+        # timm DropPath is called once per branch: two independent per-sample draws
+        self.dp = (rng.Drop(drop_path, mode=2), rng.Drop(drop_path, mode=2)) if drop_path > 0 else None
         self.norm2 = norm_layer(dim)
         self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
 
@@ -140,9 +146,13 @@ class SwinTransformerBlock3D(nn.Module):
 
     def forward(self, x, mask_matrix=None):
         B, D, H, W, C = x.shape
+        on = self.dp is not None and self.training
+        dp = (self.dp[0].spec(D * H * W), self.dp[1].spec(D * H * W)) if on else (None, None)
         o = self.forward_part1(x, mask_matrix)
-        x = Fn.linear(o, self.attn.proj.weight, self.attn.proj.bias, residual=x.reshape(-1, C))   # x + proj(o)
-        x = Fn.mlp(Fn.layer_norm(x, self.norm2), self.mlp.fc1, self.mlp.fc2, residual=x)          # x + mlp(LN2 x)
+        x = Fn.linear(o, self.attn.proj.weight, self.attn.proj.bias, residual=x.reshape(-1, C),
+                      drop=dp[0])                                                    # x + DropPath(proj(o))
+        x = Fn.mlp(Fn.layer_norm(x, self.norm2), self.mlp.fc1, self.mlp.fc2, residual=x,
+                   drop_out=dp[1])                                                      # x + DropPath(mlp(LN2 x))
         return x.view(B, D, H, W, C)
 
 

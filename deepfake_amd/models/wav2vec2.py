@@ -10,8 +10,17 @@ models/wav2vec2/modeling_wav2vec2.py (HF/ below) on HIP kernels:
   12 post-LN encoder layers       fused qkv GEMM, whole-sequence attention kernel,
                                   out_proj+residual, LN, FFN(+residual), LN (HF/:575-608)
 
-Deterministic configuration only (dropouts, LayerDrop, SpecAugment must be 0:
-constructing for training with them raises), matching the parity setup (Q12).
+Training-mode regularisers of the checkpoint config (HF/ sites, all drawn on the
+device, deepfake_amd.rng): feat_proj_dropout after the projection GEMM (:433),
+SpecAugment time masking with masked_spec_embed (:1272-1317), hidden dropout
+after the encoder-input LN (:692), attention-probability dropout inside the
+attention kernel (:458), hidden dropout after out_proj and after the FFN output
+GEMM (:596,:571), activation dropout after the FFN GELU (:568), all fused into
+the producing kernel's epilogue; LayerDrop (:700-706) as per-layer device coins:
+a dropped layer still runs (a captured graph cannot branch) but its output is
+discarded (torch.where), its gradients are zero and the fused SGD skips its
+parameters (as torch's SGD skips grad=None).  config.deterministic() turns all
+of them off (the parity setting, Q12).
 """
 import json
 
@@ -20,6 +29,8 @@ import torch.nn as nn
 from torch.nn.utils import parametrizations
 
 from .. import functional as Fn
+from .. import kernels as K
+from .. import rng
 
 
 class Wav2Vec2Config:
@@ -41,7 +52,10 @@ class Wav2Vec2Config:
         self.layer_norm_eps = kw.get("layer_norm_eps", 1e-5)
         self.do_stable_layer_norm = kw.get("do_stable_layer_norm", False)
         self.mask_time_prob = kw.get("mask_time_prob", 0.05)
+        self.mask_time_length = kw.get("mask_time_length", 10)
+        self.mask_time_min_masks = kw.get("mask_time_min_masks", 2)
         self.mask_feature_prob = kw.get("mask_feature_prob", 0.0)
+        self.apply_spec_augment = kw.get("apply_spec_augment", True)
         self.layerdrop = kw.get("layerdrop", 0.1)
         for k in ("hidden_dropout", "attention_dropout", "activation_dropout", "feat_proj_dropout"):
             setattr(self, k, kw.get(k, 0.1))
@@ -101,10 +115,12 @@ class Wav2Vec2FeatureProjection(nn.Module):
         super().__init__()
         self.layer_norm = nn.LayerNorm(config.conv_dim[-1], eps=config.layer_norm_eps)
         self.projection = nn.Linear(config.conv_dim[-1], config.hidden_size)
+        self.dropout = rng.Drop(config.feat_proj_dropout)
 
     def forward(self, x):
         n = Fn.layer_norm(x, self.layer_norm)
-        return Fn.linear(n, self.projection.weight, self.projection.bias), n
+        d = self.dropout.spec() if self.dropout.active(self.training) else None
+        return Fn.linear(n, self.projection.weight, self.projection.bias, drop=d), n
 
 
 class Wav2Vec2PositionalConvEmbedding(nn.Module):
@@ -135,9 +151,10 @@ class Wav2Vec2PositionalConvEmbedding(nn.Module):
 class Wav2Vec2Attention(nn.Module):
     """HF/:466-548: q/k/v/out projections; softmax(q k^T * hd^-0.5) v."""
 
-    def __init__(self, embed_dim, num_heads):
+    def __init__(self, embed_dim, num_heads, dropout=0.0):
         super().__init__()
         self.embed_dim, self.num_heads = embed_dim, num_heads
+        self.dropout = rng.Drop(dropout)
         self.head_dim = embed_dim // num_heads
         self.scaling = self.head_dim ** -0.5
         self.k_proj = nn.Linear(embed_dim, embed_dim)
@@ -151,7 +168,8 @@ class Wav2Vec2Attention(nn.Module):
         b = torch.cat((self.q_proj.bias, self.k_proj.bias, self.v_proj.bias))
         qkv = Fn.linear(x, w, b)
         geo = ((B, 1, 1, T), (1, 1, T), (1, 1, T), (0, 0, 0), self.num_heads, self.head_dim, self.scaling)
-        return Fn.window_attention(qkv, None, None, geo)
+        d = self.dropout.spec() if self.dropout.active(self.training) else None
+        return Fn.window_attention(qkv, None, None, geo, drop=d)
 
 
 class Wav2Vec2FeedForward(nn.Module):
@@ -161,6 +179,8 @@ class Wav2Vec2FeedForward(nn.Module):
         super().__init__()
         self.intermediate_dense = nn.Linear(config.hidden_size, config.intermediate_size)
         self.output_dense = nn.Linear(config.intermediate_size, config.hidden_size)
+        self.intermediate_dropout = rng.Drop(config.activation_dropout)
+        self.output_dropout = rng.Drop(config.hidden_dropout)
 
 
 class Wav2Vec2EncoderLayer(nn.Module):
@@ -168,17 +188,21 @@ class Wav2Vec2EncoderLayer(nn.Module):
 
     def __init__(self, config):
         super().__init__()
-        self.attention = Wav2Vec2Attention(config.hidden_size, config.num_attention_heads)
+        self.attention = Wav2Vec2Attention(config.hidden_size, config.num_attention_heads, config.attention_dropout)
+        self.dropout = rng.Drop(config.hidden_dropout)
         self.layer_norm = nn.LayerNorm(config.hidden_size, eps=config.layer_norm_eps)
         self.feed_forward = Wav2Vec2FeedForward(config)
         self.final_layer_norm = nn.LayerNorm(config.hidden_size, eps=config.layer_norm_eps)
 
     def forward(self, x, B, T):
-        a = self.attention.core(x, B, T)
-        x = Fn.layer_norm(Fn.linear(a, self.attention.out_proj.weight, self.attention.out_proj.bias, residual=x),
-                          self.layer_norm)
+        tr = self.training
         ff = self.feed_forward
-        x = Fn.mlp(x, ff.intermediate_dense, ff.output_dense, residual=x)
+        spec = lambda d: d.spec() if d.active(tr) else None   # noqa: E731
+        a = self.attention.core(x, B, T)
+        x = Fn.layer_norm(Fn.linear(a, self.attention.out_proj.weight, self.attention.out_proj.bias, residual=x,
+                                    drop=spec(self.dropout)), self.layer_norm)
+        x = Fn.mlp(x, ff.intermediate_dense, ff.output_dense, residual=x, drop_act=spec(ff.intermediate_dropout),
+                   drop_out=spec(ff.output_dropout))
         return Fn.layer_norm(x, self.final_layer_norm)
 
 
@@ -191,13 +215,31 @@ class Wav2Vec2Encoder(nn.Module):
             raise NotImplementedError("stable-layer-norm encoder")
         self.pos_conv_embed = Wav2Vec2PositionalConvEmbedding(config)
         self.layer_norm = nn.LayerNorm(config.hidden_size, eps=config.layer_norm_eps)
+        self.dropout = rng.Drop(config.hidden_dropout)
         self.layers = nn.ModuleList([Wav2Vec2EncoderLayer(config) for _ in range(config.num_hidden_layers)])
+        # LayerDrop coins: rank-independent draws (every replica drops the same layers, so the SGD skip of a
+        # dropped layer's parameters stays identical across data-parallel ranks); 1 = run, 0 = skip
+        self.layerdrop = rng.Drop(config.layerdrop, shared=True)
+        self.register_buffer("layer_keep", torch.ones(config.num_hidden_layers), persistent=False)
+
+    def param_gates(self):
+        """(parameters, device flag) pairs for the fused SGD: a layer's parameters are stepped only when its
+        LayerDrop coin kept it (training with layerdrop > 0)."""
+        if self.layerdrop.p <= 0:
+            return []
+        return [(list(l.parameters()), self.layer_keep[i:i + 1]) for i, l in enumerate(self.layers)]
 
     def forward(self, h):
         B, T, C = h.shape
-        x = Fn.layer_norm(self.pos_conv_embed.add_to(h.contiguous()), self.layer_norm).reshape(B * T, C)
-        for layer in self.layers:
-            x = layer(x, B, T)
+        d = self.dropout.spec() if self.dropout.active(self.training) else None
+        x = Fn.layer_norm(self.pos_conv_embed.add_to(h.contiguous()), self.layer_norm, drop=d).reshape(B * T, C)
+        lds = self.layerdrop.active(self.training)
+        if lds:
+            K.L.check(K.L.lib().dfk_bernoulli_flags(K.L.drop(self.layerdrop.spec(), x.device), len(self.layers),
+                                                    K.L.ptr(self.layer_keep), K.L.stream()), "bernoulli_flags")
+        for i, layer in enumerate(self.layers):
+            y = layer(x, B, T)
+            x = torch.where(self.layer_keep[i] > 0, y, x) if lds else y
         return x.view(B, T, C)
 
 
@@ -213,18 +255,22 @@ class Wav2Vec2Model(nn.Module):
             self.masked_spec_embed = nn.Parameter(torch.empty(config.hidden_size).uniform_())
         self.encoder = Wav2Vec2Encoder(config)
 
-    def _check_deterministic(self):
+        self.spec_site = rng.Drop(0.0)   # SpecAugment draws (site only)
+        if config.mask_feature_prob > 0.0:
+            raise NotImplementedError("SpecAugment feature masking (mask_feature_prob > 0)")
+
+    def _mask_hidden_states(self, h):
+        """HF/:1272-1317 time masking (training, apply_spec_augment, mask_time_prob > 0)."""
         c = self.config
-        if self.training and (c.mask_time_prob > 0 or c.mask_feature_prob > 0 or c.layerdrop > 0 or
-                              c.hidden_dropout > 0 or c.attention_dropout > 0 or c.activation_dropout > 0 or
-                              c.feat_proj_dropout > 0):
-            raise NotImplementedError("wav2vec2 training with SpecAugment/LayerDrop/dropout > 0 is not implemented on "
-                                      "the MI355X path: use config.deterministic()")
+        if not (self.training and c.apply_spec_augment and c.mask_time_prob > 0):
+            return h
+        return Fn.SpecAugmentFn.apply(h, self.masked_spec_embed, c.mask_time_prob, c.mask_time_length,
+                                      c.mask_time_min_masks, self.spec_site.spec())
 
     def forward(self, input_values, attention_mask=None, **_):
         if attention_mask is not None:
             raise NotImplementedError("attention_mask (padded batches)")
-        self._check_deterministic()
         f = self.feature_extractor(input_values)
         h, ext = self.feature_projection(f)
+        h = self._mask_hidden_states(h)
         return {"last_hidden_state": self.encoder(h), "extract_features": ext}

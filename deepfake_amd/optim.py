@@ -31,16 +31,20 @@ class FusedSGD:
         """One SGD step over the parameters that received a gradient (torch skips grad=None:
         no weight decay and no momentum for them), in as few contiguous launches as possible."""
         st = self.store
+        gates = {id(g): g for g in st.gate if g is not None}
+        gkey = [id(g) if g is not None else None for g in st.gate]
         if not any(st.touched):          # no bookkeeping (e.g. a captured replay): every parameter
-            runs = [(0, st.numel, self.first if first is None else first)]
+            f0 = self.first if first is None else first
+            runs = st.touched_runs(also=[(f0, k) for k in gkey], every=True)
         else:
-            runs = st.touched_runs(also=[not h for h in self.has_buf])
+            runs = st.touched_runs(also=[(not h, k) for h, k in zip(self.has_buf, gkey)])
             for i, t in enumerate(st.touched):
                 if t:
                     self.has_buf[i] = True
-        for s, e, f in runs:
+        # a LayerDrop-gated run is skipped on the device when its layer was dropped this step
+        for s, e, (f, k) in runs:
             K.sgd_step(st.flat[s:e], st.grad[s:e], self.buf[s:e], st.shadow[s:e] if st.shadow is not None else None,
-                       0.0, self.momentum, self.weight_decay, bool(f), lr_dev=self.lr_dev)
+                       0.0, self.momentum, self.weight_decay, bool(f), lr_dev=self.lr_dev, gate=gates.get(k))
         self.first = False
 
     def zero_grad(self):

@@ -56,6 +56,15 @@ class ParamStore:
         self.touched = [False] * len(self.params)
         for i, p in enumerate(self.params):
             p.register_post_accumulate_grad_hook(self._mark(i))
+        # device skip flags (LayerDrop): gate[i] is a 1-element fp32 tensor, 0 = leave parameter i untouched
+        self.gate = [None] * len(self.params)
+        for m in model.modules():
+            if hasattr(m, "param_gates"):
+                for ps, flag in m.param_gates():
+                    for p in ps:
+                        i = self.index.get(id(p))
+                        if i is not None:
+                            self.gate[i] = flag
         self.refresh_shadow()
 
     def _mark(self, i):
@@ -76,12 +85,12 @@ class ParamStore:
         for cb in self.listeners:
             cb(i)
 
-    def touched_runs(self, also=None):
+    def touched_runs(self, also=None, every=False):
         """Contiguous [start, end) element ranges of the flat buffers covering the touched
-        parameters (split where ``also[i]`` changes as well)."""
+        parameters (every=True: all parameters), split where ``also[i]`` changes as well."""
         runs = []
         for i, t in enumerate(self.touched):
-            if not t:
+            if not (t or every):
                 continue
             s, e = self.offsets[i], self.offsets[i] + self.params[i].numel()
             key = also[i] if also is not None else None

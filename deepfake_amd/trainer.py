@@ -21,6 +21,7 @@ import time
 import torch
 import torch.distributed as dist
 
+from . import rng
 from .ddp import GradBucketer
 from .optim import CosineAnnealingLR, FusedSGD
 from .params import ParamStore
@@ -81,6 +82,7 @@ class TrainStep:
             bucketer.track_batchnorm(model)
 
     def _fwd_bwd(self, feature, label, scale=1.0):
+        rng.advance(self.store.flat.device)   # fresh dropout / DropPath / LayerDrop / SpecAugment draws
         prob = self.model(feature)
         loss = self.lossF(prob.float().reshape(-1), label.float().reshape(-1))
         (loss * scale if scale != 1.0 else loss).backward()

@@ -26,6 +26,25 @@ extern "C" {
 #define DFK_BF16 1
 #define DFK_EINVAL (-1)
 
+/* Training-mode dropout / DropPath / LayerDrop masks, drawn by a counter-based hash inside the kernels
+ * that apply them, so the backward regenerates the forward's mask and a captured HIP graph draws new
+ * masks at every replay (the seed and step counter live in device memory; the step is advanced once per
+ * training micro-step).  Replaces nn.Dropout / F.dropout (src/utils.py:253-258, HF modeling_wav2vec2.py
+ * :434,:458,:568,:572,:604,:692), timm DropPath (video_swin_transformer.py:214,272,276;
+ * swin_transformer2d.py:240,301,304) and the LayerDrop coin (HF :700-706).
+ *   keep(draw) <=> uniform(draw) >= p; kept values are scaled by 1/(1-p).
+ *   mode 1: one draw per element (row, col); mode 2: one draw per group of group_rows rows (DropPath: the
+ *   tokens of one clip).  shared: draw from the rank-independent seed (LayerDrop flags, identical on every
+ *   data-parallel rank) instead of the per-rank one.  rng == NULL or mode == 0: no dropout. */
+typedef struct {
+  const int64_t* rng;   /* device int64[4]: per-rank seed, step, shared seed, unused */
+  int32_t mode;
+  int32_t site;         /* distinct per dropout site of the model */
+  float p;
+  int32_t group_rows;
+  int32_t shared;
+} dfk_drop;
+
 /* A 2-D operand view V(r, c), contiguous along c.
  *  plain: V(r,c) = ptr[r*ld + c]
  *  conv : V(r,c) = ptr[(r*conv_stride + c/conv_cg - conv_pad)*ld + c%conv_cg]   (0 outside [0,conv_rows))
@@ -50,7 +69,7 @@ typedef struct {
  *   :291 (PatchMerging.reduction), ModalFusion.py:16-25, HF modeling_wav2vec2.py
  *   :258-272 (conv1..6), :326-368 (pos-conv), :495-498,:556-561 (encoder linears).
  * Epilogue, in order: +bias[j]; act==1: aux<-v (if aux), v=gelu(v);
- *   act==2: v *= gelu'(aux[i,j]); +residual[i,j]; then store
+ *   act==2: v *= gelu'(aux[i,j]); v *= drop mask (row i + z*M, col j); +residual[i,j]; then store
  *   (beta: v += beta*C_old) or fp32 atomicAdd (atomic=1, for split-K / batch-summed weight grads).
  * Contract: the contiguous extent and ld of each view are multiples of 8 (bf16) / 4 (f32). */
 typedef struct {
@@ -76,6 +95,7 @@ typedef struct {
   void* ws;             /* fp32 split-K slabs, dfk_gemm_workspace(g) bytes (NULL: no automatic split) */
   float* rowsum;        /* optional, nz0 = nz1 = 1: rowsum[i] += sum_k A(i,k) (fp32) — the bias gradient
                            of a Linear when A = dy^T, computed by one extra MFMA against a ones operand */
+  dfk_drop drop;        /* dropout / DropPath of the output before the residual add (bf16/f32 C only) */
 } dfk_gemm_args;
 int dfk_gemm(const dfk_gemm_args* g, hipStream_t stream);
 /* Bytes of scratch dfk_gemm wants in g->ws: grids too small to fill the chip (the
@@ -88,16 +108,21 @@ int dfk_colsum(const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld,
 
 /* LayerNorm over the last dim C of `rows` rows (nn.LayerNorm / F.layer_norm,
  * video_swin_transformer.py:209,215,292,548,678; HF :424,:586-588,:661).
- * y = (x-mean)*rstd*w + b; saves mean/rstd (fp32) for the backward. */
+ * y = (x-mean)*rstd*w + b; saves mean/rstd (fp32) for the backward.
+ * Optional: y = residual + drop(LN(x)) — the SwinV2 post-norm residual x + DropPath(LN(a))
+ * (swin_transformer2d.py:301,304) and LN -> dropout of the wav2vec2 encoder input (HF :691-692);
+ * residual / drop may be NULL. */
 int dfk_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
-                      int64_t rows, int32_t C, float eps, int dtype, hipStream_t stream);
-/* dx (=, or += when accumulate) ; dw, db accumulate (+=).  ws: fp32 scratch of
+                      int64_t rows, int32_t C, float eps, int dtype, const void* residual, const dfk_drop* drop,
+                      hipStream_t stream);
+/* dx (=, or += when accumulate) ; dw, db accumulate (+=); drop (may be NULL): the forward's mask applied
+ * to dy first (the gradient of drop(LN(x))).  ws: fp32 scratch of
  * dfk_layernorm_bwd_workspace(rows, C) bytes for per-workgroup dw/db partials,
  * column-summed by a second pass; NULL: fp32 atomics per workgroup and channel
  * (same-address contention: slow when many workgroups share few channels). */
 int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                       void* dx, float* dw, float* db, int64_t rows, int32_t C, int accumulate, int dtype,
-                      float* ws, hipStream_t stream);
+                      float* ws, const dfk_drop* drop, hipStream_t stream);
 int64_t dfk_layernorm_bwd_workspace(int64_t rows, int32_t C);
 
 /* Windowed multi-head attention core on token-major buffers (no window
@@ -138,6 +163,9 @@ typedef struct {
   int32_t dtype;
   float scale;
   void* tab;
+  dfk_drop drop;        /* attention-probability dropout (mode 1, bf16 table path only; row = query,
+                           col = key of the (clip, window, head) unit): HF eager_attention_forward's
+                           nn.functional.dropout(attn_weights, p=attention_dropout) (HF :458) */
 } dfk_wattn_args;
 int dfk_wattn_fwd(const dfk_wattn_args* a, hipStream_t stream);
 int64_t dfk_wattn_table_workspace(const dfk_wattn_args* a);
@@ -246,7 +274,28 @@ int dfk_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, int dtype
  * memory when lr_dev != NULL (graph-replay safe CosineAnnealingLR). */
 int dfk_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow, int64_t n,
                  const float* lr_dev, float lr, float momentum, float weight_decay, int first_step,
-                 hipStream_t stream);
+                 const float* gate, hipStream_t stream);
+/* gate (above; may be NULL): device flag, the step is skipped when *gate == 0 — the parameters of a
+ * LayerDrop-skipped wav2vec2 layer have grad None in the reference and torch's SGD leaves them (and
+ * their momentum) untouched. */
+
+/* y = x * mask / (1 - p) over [rows, cols] (row stride ld; y may alias x): nn.Dropout / DropPath as a
+ * standalone pass, and the backward of every fused dropout site (the same mask applied to the gradient). */
+int dfk_dropout(const void* x, void* y, int64_t rows, int32_t cols, int64_t ld, const dfk_drop* drop, int dtype,
+                hipStream_t stream);
+/* out[i] = keep(draw i) ? 1 : 0 for i < n (fp32): the per-layer LayerDrop coins of the wav2vec2 encoder
+ * (HF :700-706: skip layer when rand < layerdrop), drawn on the device so a replayed graph re-draws them. */
+int dfk_bernoulli_flags(const dfk_drop* drop, int32_t n, float* out, hipStream_t stream);
+/* SpecAugment time masking (HF Wav2Vec2Model._mask_hidden_states :1272-1317 with _compute_mask_indices
+ * :101-218, no attention mask): per clip, num = max(min_masks, int(mask_prob*T/mask_length + eps)) (eps one
+ * uniform draw per call, num clamped as HF does) distinct span starts drawn uniformly from [0, T-mask_length],
+ * frames [start, start+mask_length) masked; out = h with masked frames replaced by embed [C].  mask [B,T] uint8
+ * is written for the backward.  bwd: dx = dy with masked frames zeroed, dembed [C] fp32 += sum of their dy. */
+int dfk_spec_augment_fwd(const void* h, void* out, uint8_t* mask, const void* embed, int32_t B, int32_t T,
+                         int32_t C, float mask_prob, int32_t mask_length, int32_t min_masks, const dfk_drop* drop,
+                         int dtype, hipStream_t stream);
+int dfk_spec_augment_bwd(const void* dy, void* dx, const uint8_t* mask, float* dembed, int32_t B, int32_t T,
+                         int32_t C, int dtype, hipStream_t stream);
 
 /* Frame normalisation on the device: T.ToTensor() + T.Normalize(mean, std) of
  * data/data_process.py:55-69 on decoded RGB frames (src/utils.py:22-39): src uint8 [frames, H, W, 3]

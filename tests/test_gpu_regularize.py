@@ -1,0 +1,241 @@
+"""GPU: training-mode regularisers (dropout, DropPath, attention dropout, LayerDrop, SpecAugment).
+
+Every mask is a counter-based hash evaluated inside the kernel that applies it (include/dfk.h dfk_drop,
+deepfake_amd/rng.py).  The tests check (a) mask statistics against the reference's distributions
+(nn.Dropout / timm DropPath: Bernoulli(1-p) scaled 1/(1-p); HF _compute_mask_indices span counts),
+(b) that every fused site applies exactly the mask dfk_dropout reproduces (so forward and backward
+agree), by comparing the fused kernels with plain torch fp32 references that use that mask, and (c)
+that the masks change with the step counter and not with anything else.  Seeded: statistics are checked
+with bounds several standard deviations wide.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from deepfake_amd import functional as Fn
+    from deepfake_amd import kernels as K
+    from deepfake_amd import rng
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12)).item()
+
+
+def mask_of(spec, rows, cols, dtype=torch.float32):
+    """The mask a spec applies to a [rows, cols] output: dfk_dropout of ones (= keep / (1-p) or 0)."""
+    return K.dropout(torch.ones(rows, cols, device=DEV, dtype=dtype), spec)
+
+
+@pytest.mark.parametrize("p", [0.1, 0.5])
+def test_dropout_statistics_and_step(p):
+    d = rng.Drop(p)
+    m = mask_of(d.spec(), 2048, 768)
+    keep = (m != 0).float()
+    frac = 1 - keep.mean().item()
+    n = m.numel()
+    assert abs(frac - p) < 6 * math.sqrt(p * (1 - p) / n)
+    assert torch.allclose(m[m != 0], torch.full_like(m[m != 0], 1 / (1 - p)))
+    assert torch.equal(m, mask_of(d.spec(), 2048, 768))                  # same step: same mask
+    rng.advance(DEV)
+    m2 = mask_of(d.spec(), 2048, 768)
+    assert not torch.equal(m, m2)                                        # next step: new mask
+    assert abs((m2 != 0).float().mean().item() - (1 - p)) < 6 * math.sqrt(p * (1 - p) / n)
+    other = mask_of(rng.Drop(p).spec(), 2048, 768)                        # another site: independent
+    agree = ((other != 0) == (m2 != 0)).float().mean().item()
+    assert abs(agree - (p * p + (1 - p) ** 2)) < 0.01
+    # columns and rows are not correlated: per-column keep rates all near 1-p
+    col = (m2 != 0).float().mean(0)
+    assert (col - (1 - p)).abs().max().item() < 6 * math.sqrt(p * (1 - p) / 2048)
+
+
+def test_droppath_groups():
+    d = rng.Drop(0.2, mode=2)
+    rows_per = 392
+    m = mask_of(d.spec(rows_per), 4000 * rows_per // 100, 96)
+    g = m.view(-1, rows_per, 96)
+    first = g[:, :1, :1]
+    assert torch.equal(g, first.expand_as(g))                             # one draw per clip
+    frac = (first == 0).float().mean().item()
+    assert abs(frac - 0.2) < 6 * math.sqrt(0.2 * 0.8 / first.numel())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mode,M,N,Kd", [(1, 1000, 288, 96), (2, 20000, 96, 384), (1, 1592, 768, 3072),
+                                         (2, 1568, 512, 2048)])
+def test_linear_dropout_epilogue(dt, mode, M, N, Kd):
+    """y = residual + drop(x W^T + b) on the tiled, split-K and weight-resident GEMMs; the backward mask."""
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.randn(M, Kd, device=DEV, generator=g).to(dt)
+    w = (torch.randn(N, Kd, device=DEV, generator=g) / math.sqrt(Kd)).to(dt)
+    b = torch.randn(N, device=DEV, generator=g).to(dt)
+    r = torch.randn(M, N, device=DEV, generator=g).to(dt)
+    spec = rng.Drop(0.3, mode=mode).spec(M // 8 if mode == 2 else 1)
+    y = K.linear(x, w, b, residual=r, drop=spec)
+    m = mask_of(spec, M, N)
+    ref = (x.float() @ w.float().t() + b.float()) * m + r.float()
+    assert rel(y, ref) < (2e-2 if dt == torch.bfloat16 else 2e-5)
+    # GELU + dropout (FFN activation dropout) and the dGELU backward with the same mask
+    aux = torch.empty(M, N, device=DEV, dtype=dt)
+    h = K.linear(x, w, b, act=1, aux=aux, drop=spec)
+    pre = x.float() @ w.float().t() + b.float()
+    assert rel(h, torch.nn.functional.gelu(pre) * m) < (2e-2 if dt == torch.bfloat16 else 2e-5)
+    dy = torch.randn(M, Kd, device=DEV, generator=g).to(dt)
+    w2 = (torch.randn(Kd, N, device=DEV, generator=g) / math.sqrt(N)).to(dt)
+    dpre = K.linear_dx(dy, w2, act=2, aux=aux, drop=spec)
+    pre_t = aux.float().requires_grad_(True)
+    (torch.nn.functional.gelu(pre_t) * m * (dy.float() @ w2.float())).sum().backward()
+    assert rel(dpre, pre_t.grad) < (3e-2 if dt == torch.bfloat16 else 1e-4)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_layernorm_residual_dropout(dt, mode):
+    """y = residual + drop(LN(x)) and its backward (SwinV2 post-norm DropPath; wav2vec2 LN -> dropout)."""
+    rows, C = 3136, 256
+    g = torch.Generator(device=DEV).manual_seed(2)
+    x = torch.randn(rows, C, device=DEV, generator=g).to(dt)
+    res = torch.randn(rows, C, device=DEV, generator=g).to(dt)
+    ln = torch.nn.LayerNorm(C).to(DEV)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    spec = rng.Drop(0.25, mode=mode).spec(196)
+    xr = x.detach().clone().requires_grad_(True)
+    rr = res.detach().clone().requires_grad_(True)
+    y = Fn.LayerNormFn.apply(xr, ln.weight.to(dt), ln.bias.to(dt), 1e-5, rr, spec)
+    m = mask_of(spec, rows, C)
+    xf = x.float().requires_grad_(True)
+    ref = res.float() + torch.nn.functional.layer_norm(xf, (C,), ln.weight, ln.bias) * m
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-5
+    assert rel(y, ref) < tol
+    dy = torch.randn(rows, C, device=DEV, generator=g).to(dt)
+    y.backward(dy)
+    ref.backward(dy.float())
+    assert rel(xr.grad, xf.grad) < (5e-2 if dt == torch.bfloat16 else 1e-4)
+    assert rel(rr.grad, dy) == 0.0
+
+
+def _w2v_attention_ref(qkv, B, T, heads, hd, m):
+    C = heads * hd
+    q, k, v = (qkv.float()[:, i * C:(i + 1) * C].reshape(B, T, heads, hd).transpose(1, 2) for i in range(3))
+    p = torch.softmax(q @ k.transpose(-1, -2) * hd ** -0.5, dim=-1)
+    return ((p * m) @ v).transpose(1, 2).reshape(B * T, C)
+
+
+@pytest.mark.parametrize("T,heads,hd", [(199, 12, 64), (49, 2, 64), (96, 3, 32)])
+def test_attention_dropout(T, heads, hd):
+    """HF eager_attention_forward with attention dropout (:458): O = (softmax(QK^T s) * Z) V; the kernel's
+    forward and all three input gradients against a torch fp32 reference using the kernel's own mask."""
+    B = 4
+    C = heads * hd
+    g = torch.Generator(device=DEV).manual_seed(3)
+    qkv = (torch.randn(B * T, 3 * C, device=DEV, generator=g) * 0.5).to(torch.bfloat16)
+    spec = rng.Drop(0.1).spec()
+    Np = -(-T // 32) * 32
+    z = mask_of(spec, B * heads * Np, Np).view(B, heads, Np, Np)[:, :, :T, :T]
+    geo = ((B, 1, 1, T), (1, 1, T), (1, 1, T), (0, 0, 0), heads, hd, hd ** -0.5)
+    x = qkv.detach().clone().requires_grad_(True)
+    o = Fn.window_attention(x, None, None, geo, drop=spec)
+    xf = qkv.float().requires_grad_(True)
+    ref = _w2v_attention_ref(xf, B, T, heads, hd, z)
+    assert rel(o, ref) < 2e-2
+    frac = (z == 0).float().mean().item()
+    assert abs(frac - 0.1) < 0.02
+    do = torch.randn(B * T, C, device=DEV, generator=g).to(torch.bfloat16)
+    o.backward(do)
+    ref.backward(do.float())
+    for i in range(3):
+        assert rel(x.grad[:, i * C:(i + 1) * C], xf.grad[:, i * C:(i + 1) * C]) < 4e-2, i
+    # p = 0 spec leaves the attention untouched
+    o0 = Fn.window_attention(qkv, None, None, geo, drop=rng.Drop(0.0).spec())
+    o1 = Fn.window_attention(qkv, None, None, geo)
+    assert torch.equal(o0, o1)
+
+
+def test_spec_augment():
+    """HF _compute_mask_indices at wav2vec2-base settings (mask_time_prob 0.05, length 10, min_masks 2):
+    T = 199 -> 2 distinct span starts per clip, spans of 10 frames (they may overlap)."""
+    B, T, C = 64, 199, 768
+    g = torch.Generator(device=DEV).manual_seed(4)
+    h = torch.randn(B, T, C, device=DEV, generator=g).to(torch.bfloat16)
+    emb = torch.randn(C, device=DEV, generator=g).to(torch.bfloat16)
+    spec = rng.Drop(0.0).spec()
+    out, mask = K.spec_augment_fwd(h, emb, 0.05, 10, 2, spec)
+    mk = mask.bool()
+    counts = mk.sum(1)
+    assert ((counts >= 10) & (counts <= 20)).all()
+    assert (counts == 20).float().mean().item() > 0.8          # non-overlapping spans are the common case
+    for b in range(B):
+        idx = mk[b].nonzero().flatten().tolist()
+        runs = 1 + sum(1 for i, j in zip(idx, idx[1:]) if j != i + 1)
+        assert 1 <= runs <= 2
+    assert torch.equal(out[mk], emb.expand(int(mk.sum()), C))
+    assert torch.equal(out[~mk], h[~mk])
+    starts = torch.cat([mk[:, :1].int(), (mk[:, 1:].int() - mk[:, :-1].int()).clamp_min(0)], 1).nonzero()[:, 1]
+    assert starts.float().mean().item() == pytest.approx((T - 10) / 2, abs=25)   # uniform over [0, 190)
+    # backward: masked frames get no gradient, the embedding gets their sum
+    dy = torch.randn(B, T, C, device=DEV, generator=g).to(torch.bfloat16)
+    de = torch.zeros(C, device=DEV)
+    dx = K.spec_augment_bwd(dy, mask, de)
+    assert torch.equal(dx[mk], torch.zeros_like(dx[mk]))
+    assert torch.equal(dx[~mk], dy[~mk])
+    assert rel(de, dy.float()[mk].sum(0)) < 1e-5
+    rng.advance(DEV)
+    _, mask2 = K.spec_augment_fwd(h, emb, 0.05, 10, 2, spec)
+    assert not torch.equal(mask, mask2)
+
+
+def test_layerdrop_flags_and_sgd_gate():
+    d = rng.Drop(0.1, shared=True)
+    flags = K.bernoulli_flags(d.spec(), 100000, DEV)
+    assert abs((flags == 0).float().mean().item() - 0.1) < 0.006
+    # the SGD gate: a gated span is left untouched (param and momentum) when its flag is 0
+    n = 1024
+    p = torch.randn(n, device=DEV)
+    gr = torch.randn(n, device=DEV)
+    buf = torch.zeros(n, device=DEV)
+    p0 = p.clone()
+    K.sgd_step(p, gr, buf, None, 0.1, 0.9, 0.05, True, gate=torch.zeros(1, device=DEV))
+    assert torch.equal(p, p0) and torch.equal(buf, torch.zeros_like(buf))
+    K.sgd_step(p, gr, buf, None, 0.1, 0.9, 0.05, True, gate=torch.ones(1, device=DEV))
+    assert rel(p, p0 - 0.1 * (gr + 0.05 * p0)) < 1e-6
+
+
+def test_fused_c1_regularized_step():
+    """The C1 fused model with the reference's regularisers trains (finite loss, gradients everywhere the
+    reference has them), its masks change from step to step, and eval mode is the deterministic model."""
+    from deepfake_amd.ddp import GradBucketer
+    from deepfake_amd.models.fused import build_fused
+    from deepfake_amd.optim import FusedSGD
+    from deepfake_amd.params import ParamStore
+    from deepfake_amd.trainer import TrainStep
+    from oracle.fill import named_fill_, synthetic_inputs
+    torch.manual_seed(0)
+    m = named_fill_(build_fused("c1", compute_dtype=torch.bfloat16, regularize=True), 7).cuda()
+    ref = named_fill_(build_fused("c1", compute_dtype=torch.bfloat16, regularize=False), 7).cuda()
+    video, mel, wave, label = synthetic_inputs(2, 8, 112, 112, 1, seed=5)
+    feat = (video.cuda(), mel.cuda(), wave.cuda())
+    m.eval()
+    ref.eval()
+    with torch.no_grad():
+        za = m.head(m.vExtract(feat[0]), m.aExtract(feat[1]), m.paExtract.wav_model(feat[2])["last_hidden_state"]
+                    .float().mean(1))
+        zb = ref.head(ref.vExtract(feat[0]), ref.aExtract(feat[1]), ref.paExtract.wav_model(feat[2])["last_hidden_state"]
+                      .float().mean(1))
+    assert rel(za, zb) < 1e-6         # eval: no regulariser is active in the trunks (Audio2D's is bypassed here)
+    m.train()
+    store = ParamStore(m, torch.bfloat16)
+    step = TrainStep(m, store, FusedSGD(store, 1e-3, 0.9, 0.05), GradBucketer(store), graph=False)
+    losses = []
+    for _ in range(3):
+        loss, prob = step(feat, label.cuda())
+        losses.append(loss.item())
+        assert torch.isfinite(store.flat).all()
+    assert all(math.isfinite(v) for v in losses)
+    assert len(set(losses)) == 3
