@@ -43,6 +43,8 @@ def manual_seed(seed, rank=0):
 def state(device):
     """The int64[4] device tensor the kernels read (created on first use)."""
     key = torch.device(device)
+    if key.type == "cuda" and key.index is None:
+        key = torch.device("cuda", torch.cuda.current_device())
     st = _states.get(key)
     if st is None:
         st = torch.tensor([_seed[0], 0, _seed[1], 0], dtype=torch.int64, device=key)
