@@ -91,8 +91,10 @@ SIGNATURES = {
     "dfk_rowmean": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],
     "dfk_cast": [_VP, C.c_int, _VP, C.c_int, _I64, _VP],
     "dfk_gelu_bwd": [_VP, _VP, _VP, _I64, C.c_int, _VP],
-    "dfk_cosine_qk_fwd": [_VP, _VP, _VP, _I64, C.c_int, C.c_int, C.c_int, _VP],
-    "dfk_cosine_qk_bwd": [_VP, _VP, _VP, _VP, _VP, _I64, C.c_int, C.c_int, C.c_int, _VP],
+    "dfk_cosine_qk_fwd": [_VP, _VP, _VP, _F, _I64, C.c_int, C.c_int, C.c_int, _VP],
+    "dfk_cosine_qk_bwd": [_VP, _VP, _VP, _VP, _F, _VP, _I64, C.c_int, C.c_int, C.c_int, _VP],
+    "dfk_cpb_bias_fwd": [_VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],
+    "dfk_cpb_bias_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],
     "dfk_w2v_conv0_fwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP],
     "dfk_w2v_conv0_bwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _VP, _VP, _VP, _VP],
     "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP, _VP],

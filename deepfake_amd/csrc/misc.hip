@@ -184,7 +184,8 @@ __device__ __forceinline__ float group_sum(float v) {
 
 template <typename T, int G>
 __global__ __launch_bounds__(256) void cosine_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out,
-                                                         const float* __restrict__ scale, long rows, int heads) {
+                                                         const float* __restrict__ logit, float max_log, long rows,
+                                                         int heads) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long grp = idx / G;
   const int l = (int)(idx % G);
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(256) void cosine_fwd_kernel(const T* __restrict__ q
   for (int e = 0; e < 8; ++e) { nq += q[e] * q[e]; nk += k[e] * k[e]; }
   nq = group_sum<G>(nq);
   nk = group_sum<G>(nk);
-  const float iq = scale[h] / fmaxf(sqrtf(nq), 1e-12f), ik = 1.f / fmaxf(sqrtf(nk), 1e-12f);
+  const float iq = __expf(fminf(logit[h], max_log)) / fmaxf(sqrtf(nq), 1e-12f), ik = 1.f / fmaxf(sqrtf(nk), 1e-12f);
 #pragma unroll
   for (int e = 0; e < 8; ++e) { q[e] *= iq; k[e] *= ik; }
   if (ok) {
@@ -212,11 +213,13 @@ __global__ __launch_bounds__(256) void cosine_fwd_kernel(const T* __restrict__ q
   }
 }
 
-// backward: dq = (s*dq' - qh*(qh . s*dq'))/|q| ; dk likewise (s = 1) ; dv = dv' ; dscale[h] += qh . dq'
+// backward: dq = (s*dq' - qh*(qh . s*dq'))/|q| ; dk likewise (s = 1) ; dv = dv' ;
+// dlogit[h] += (qh . dq') * s * [logit <= max_log]   (s = exp(clamp(logit, max=max_log)))
 template <typename T, int G>
 __global__ __launch_bounds__(256) void cosine_bwd_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
-                                                         T* __restrict__ dqkv, const float* __restrict__ scale,
-                                                         float* __restrict__ dscale, long rows, int heads) {
+                                                         T* __restrict__ dqkv, const float* __restrict__ logit,
+                                                         float max_log, float* __restrict__ dlogit, long rows,
+                                                         int heads) {
   __shared__ float red[64];
   if (threadIdx.x < 64) red[threadIdx.x] = 0.f;
   __syncthreads();
@@ -240,7 +243,7 @@ __global__ __launch_bounds__(256) void cosine_bwd_kernel(const T* __restrict__ q
     n2 = group_sum<G>(n2);
     xd = group_sum<G>(xd);
     const float n = sqrtf(n2), inv = 1.f / fmaxf(n, 1e-12f);
-    const float sc = part == 0 ? scale[h] : 1.f;
+    const float sc = part == 0 ? __expf(fminf(logit[h], max_log)) : 1.f;
     const float dot = xd * inv;   // xhat . dq'
     if (part == 0) dsq = dot;
     const bool clamped = n <= 1e-12f;
@@ -259,20 +262,23 @@ __global__ __launch_bounds__(256) void cosine_bwd_kernel(const T* __restrict__ q
     if (l == 0) atomicAdd(&red[h & 63], dsq);
   }
   __syncthreads();
-  if (threadIdx.x < heads && threadIdx.x < 64 && red[threadIdx.x] != 0.f) atomicAdd(dscale + threadIdx.x, red[threadIdx.x]);
+  if (threadIdx.x < heads && threadIdx.x < 64 && red[threadIdx.x] != 0.f) {
+    const float lg = logit[threadIdx.x];
+    if (lg <= max_log) atomicAdd(dlogit + threadIdx.x, red[threadIdx.x] * __expf(lg));
+  }
 }
 
 }  // namespace
 
-extern "C" int dfk_cosine_qk_fwd(const void* qkv, void* out, const float* scale, int64_t rows, int heads, int hd,
-                                 int dtype, hipStream_t s) {
-  if (!qkv || !out || !scale || heads <= 0 || heads > 64 || (hd != 32 && hd != 64)) return DFK_EINVAL;
+extern "C" int dfk_cosine_qk_fwd(const void* qkv, void* out, const float* logit_scale, float max_log, int64_t rows,
+                                 int heads, int hd, int dtype, hipStream_t s) {
+  if (!qkv || !out || !logit_scale || heads <= 0 || heads > 64 || (hd != 32 && hd != 64)) return DFK_EINVAL;
   if (reinterpret_cast<uintptr_t>(qkv) % 16 || reinterpret_cast<uintptr_t>(out) % 16) return DFK_EINVAL;
   const long n = rows * heads * (hd / 8);
   if (n <= 0) return 0;
   const dim3 grid((unsigned)((n + 255) / 256));
-#define COS_F(T, G) hipLaunchKernelGGL((cosine_fwd_kernel<T, G>), grid, dim3(256), 0, s, (const T*)qkv, (T*)out, scale, \
-                                       (long)rows, heads)
+#define COS_F(T, G) hipLaunchKernelGGL((cosine_fwd_kernel<T, G>), grid, dim3(256), 0, s, (const T*)qkv, (T*)out, \
+                                       logit_scale, max_log, (long)rows, heads)
   if (dtype == DFK_BF16) { if (hd == 32) COS_F(bf16raw, 4); else COS_F(bf16raw, 8); }
   else { if (hd == 32) COS_F(float, 4); else COS_F(float, 8); }
 #undef COS_F
@@ -280,9 +286,9 @@ extern "C" int dfk_cosine_qk_fwd(const void* qkv, void* out, const float* scale,
   return 0;
 }
 
-extern "C" int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, const float* scale, float* dscale,
-                                 int64_t rows, int heads, int hd, int dtype, hipStream_t s) {
-  if (!qkv || !dout || !dqkv || !scale || !dscale || heads <= 0 || heads > 64 || (hd != 32 && hd != 64))
+extern "C" int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, const float* logit_scale, float max_log,
+                                 float* dlogit_scale, int64_t rows, int heads, int hd, int dtype, hipStream_t s) {
+  if (!qkv || !dout || !dqkv || !logit_scale || !dlogit_scale || heads <= 0 || heads > 64 || (hd != 32 && hd != 64))
     return DFK_EINVAL;
   if (reinterpret_cast<uintptr_t>(qkv) % 16 || reinterpret_cast<uintptr_t>(dout) % 16 ||
       reinterpret_cast<uintptr_t>(dqkv) % 16)
@@ -291,7 +297,7 @@ extern "C" int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, 
   if (n <= 0) return 0;
   const dim3 grid((unsigned)((n + 255) / 256));
 #define COS_B(T, G) hipLaunchKernelGGL((cosine_bwd_kernel<T, G>), grid, dim3(256), 0, s, (const T*)qkv, (const T*)dout, \
-                                       (T*)dqkv, scale, dscale, (long)rows, heads)
+                                       (T*)dqkv, logit_scale, max_log, dlogit_scale, (long)rows, heads)
   if (dtype == DFK_BF16) { if (hd == 32) COS_B(bf16raw, 4); else COS_B(bf16raw, 8); }
   else { if (hd == 32) COS_B(float, 4); else COS_B(float, 8); }
 #undef COS_B

@@ -109,6 +109,67 @@ def linear(x, weight, bias=None, act=0, residual=None, drop=None):
     return y.view(*shp[:-1], weight.shape[0])
 
 
+class GroupLinearFn(torch.autograd.Function):
+    """y = x W^T + b where W (and b) are ParamStore adjacency groups (several parameters back to back, b
+    possibly with zero gaps): the GEMMs read the flat master / bf16 shadow views in place and the backward
+    writes dW / db straight into the flat gradient view, then reports every member ready."""
+
+    @staticmethod
+    def forward(ctx, x, st, wspan, wshape, bspan, *params):
+        dt = x.dtype
+        src = st.shadow if (dt == torch.bfloat16 and st.shadow is not None) else st.flat
+        if src.dtype != dt:
+            raise RuntimeError("GroupLinearFn: compute dtype has no flat view")
+        W = src[wspan[0]:wspan[0] + wspan[1]].view(wshape)
+        B = src[bspan[0]:bspan[0] + bspan[1]] if bspan is not None else None
+        y = K.linear(x, W, B)
+        for i, p in enumerate(params):
+            grad_use(ctx, 5 + i, p)
+        ctx.save_for_backward(x, *params)
+        ctx.st, ctx.wspan, ctx.wshape, ctx.bspan = st, wspan, wshape, bspan
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, *params = ctx.saved_tensors
+        st, (wo, wn), wshape, bspan = ctx.st, ctx.wspan, ctx.wshape, ctx.bspan
+        dy = dy.contiguous()
+        src = st.shadow if (x.dtype == torch.bfloat16 and st.shadow is not None) else st.flat
+        dx = K.linear_dx(dy, src[wo:wo + wn].view(wshape)) if ctx.needs_input_grad[0] else None
+        if any(p.grad is None for p in params):
+            st.rebind_grads()
+        db = st.grad[bspan[0]:bspan[0] + bspan[1]] if bspan is not None else None
+        K.linear_dw(dy, x, st.grad[wo:wo + wn].view(wshape), db=db)
+        for p in params:
+            grad_done(p, None)
+        return (dx, None, None, None, None) + (None,) * len(params)
+
+
+def linear_group(x, weights, biases=None):
+    """nn.Linear over concatenated parameters: W = cat(weights) [sum N_i, K], b = cat(biases) with int
+    entries of `biases` standing for zero gaps (SwinV2's qkv bias = cat(q_bias, 0, v_bias),
+    swin_transformer2d.py:151-153; wav2vec2's separate q/k/v projections, HF :495-498).  With a ParamStore
+    that laid the groups out adjacently (module.flat_groups()) nothing is concatenated; otherwise the
+    reference's torch.cat."""
+    shp = x.shape
+    x2 = rows2d(x).contiguous()
+    st = _store(weights[0])
+    if st is not None:
+        ws = st.group_span(list(weights))
+        bs = st.group_span(list(biases)) if biases is not None else None
+        if ws is not None and (biases is None or bs is not None):
+            wshape = (sum(w.shape[0] for w in weights), weights[0].shape[1])
+            ps = list(weights) + [b for b in (biases or []) if not isinstance(b, int)]
+            y = GroupLinearFn.apply(x2, st, ws, wshape, bs, *ps)
+            return y.view(*shp[:-1], wshape[0])
+    W = torch.cat(list(weights)) if len(weights) > 1 else weights[0]
+    b = None
+    if biases is not None:
+        b = torch.cat([torch.zeros(e, device=x.device, dtype=weights[0].dtype) if isinstance(e, int) else e
+                       for e in biases])
+    return linear(x, W, b)
+
+
 class MlpFn(torch.autograd.Function):
     """residual + drop_out(fc2(drop_act(gelu(fc1(x))))) — src/utils.py:242-260 Mlp / HF Wav2Vec2FeedForward
     (:551-573: activation dropout after the GELU, hidden dropout after fc2) fused with the block residual
@@ -410,28 +471,61 @@ class PosConvFn(torch.autograd.Function):
 
 
 class CosineQKFn(torch.autograd.Function):
-    """SwinV2 cosine attention prologue: [rows, 3C] -> (normalize(q)*scale[h], normalize(k), v)."""
+    """SwinV2 cosine attention prologue: [rows, 3C] -> (normalize(q)*scale[h], normalize(k), v) with
+    scale = exp(clamp(logit_scale, max=max_log)) computed in the kernel from the fp32 parameter
+    (swin_transformer2d.py:154-157); the logit_scale gradient is accumulated directly."""
 
     @staticmethod
-    def forward(ctx, qkv, scale, heads, hd):
+    def forward(ctx, qkv, logit_scale, heads, hd, max_log):
         out = torch.empty_like(qkv)
-        s = scale.detach().float().contiguous()
-        K.L.check(K.L.lib().dfk_cosine_qk_fwd(K.L.ptr(qkv), K.L.ptr(out), K.L.ptr(s), qkv.shape[0], heads, hd,
-                                              K.L.dt(qkv), K.L.stream()), "cosine_qk_fwd")
-        ctx.save_for_backward(qkv, s)
-        ctx.hd = hd
+        ls = logit_scale.detach()
+        if ls.dtype != torch.float32 or not ls.is_contiguous():
+            ls = ls.float().contiguous()
+        K.L.check(K.L.lib().dfk_cosine_qk_fwd(K.L.ptr(qkv), K.L.ptr(out), K.L.ptr(ls), float(max_log), qkv.shape[0],
+                                              heads, hd, K.L.dt(qkv), K.L.stream()), "cosine_qk_fwd")
+        grad_use(ctx, 1, logit_scale)
+        ctx.save_for_backward(qkv, ls, logit_scale)
+        ctx.hd, ctx.max_log = hd, max_log
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, s = ctx.saved_tensors
-        heads = s.numel()
+        qkv, ls, logit_scale = ctx.saved_tensors
+        heads = ls.numel()
         dqkv = torch.empty_like(qkv)
-        ds = torch.zeros(heads, device=qkv.device)
-        K.L.check(K.L.lib().dfk_cosine_qk_bwd(K.L.ptr(qkv), K.L.ptr(dout.contiguous()), K.L.ptr(dqkv), K.L.ptr(s),
-                                              K.L.ptr(ds), qkv.shape[0], heads, ctx.hd, K.L.dt(qkv), K.L.stream()),
-                  "cosine_qk_bwd")
-        return dqkv, ds, None, None
+        dls = grad_sink(logit_scale) if logit_scale.dtype == torch.float32 else torch.zeros_like(ls)
+        K.L.check(K.L.lib().dfk_cosine_qk_bwd(K.L.ptr(qkv), K.L.ptr(dout.contiguous()), K.L.ptr(dqkv), K.L.ptr(ls),
+                                              float(ctx.max_log), K.L.ptr(dls), qkv.shape[0], heads, ctx.hd,
+                                              K.L.dt(qkv), K.L.stream()), "cosine_qk_bwd")
+        return dqkv, grad_done(logit_scale, dls.view_as(logit_scale)), None, None, None
+
+
+class CPBBiasFn(torch.autograd.Function):
+    """SwinV2 relative-position bias table 16*sigmoid(cpb_mlp(relative_coords_table)) -> [L, heads] fp32
+    (swin_transformer2d.py:159-162) in one kernel each way (dfk_cpb_bias_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, coords, w1, b1, w2):
+        L, heads, hidden = coords.numel() // 2, w2.shape[0], w2.shape[1]
+        c = coords.detach().float().reshape(L, 2).contiguous()
+        W1, B1, W2 = (t.detach().float().contiguous() for t in (w1, b1, w2))
+        out = torch.empty(L, heads, device=coords.device, dtype=torch.float32)
+        K.L.check(K.L.lib().dfk_cpb_bias_fwd(K.L.ptr(c), K.L.ptr(W1), K.L.ptr(B1), K.L.ptr(W2), K.L.ptr(out), L,
+                                             hidden, heads, K.L.stream()), "cpb_bias_fwd")
+        for i, p in enumerate((w1, b1, w2)):
+            grad_use(ctx, 1 + i, p)
+        ctx.save_for_backward(c, W1, B1, W2, out, w1, b1, w2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        c, W1, B1, W2, out, w1, b1, w2 = ctx.saved_tensors
+        L, heads, hidden = out.shape[0], W2.shape[0], W2.shape[1]
+        d1, db, d2 = grad_sink(w1), grad_sink(b1), grad_sink(w2)
+        K.L.check(K.L.lib().dfk_cpb_bias_bwd(K.L.ptr(c), K.L.ptr(W1), K.L.ptr(B1), K.L.ptr(W2), K.L.ptr(out),
+                                             K.L.ptr(dout.float().contiguous()), K.L.ptr(d1), K.L.ptr(db), K.L.ptr(d2),
+                                             L, hidden, heads, K.L.stream()), "cpb_bias_bwd")
+        return None, grad_done(w1, d1), grad_done(b1, db), grad_done(w2, d2)
 
 
 class PatchEmbedLNFn(torch.autograd.Function):

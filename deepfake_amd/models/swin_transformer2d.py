@@ -89,16 +89,22 @@ class WindowAttention(nn.Module):
 
     def bias_table(self):
         """[(2Wh-1)(2Ww-1), nH] fp32 = 16*sigmoid(cpb_mlp(coords)) (:159-164), indexed in-kernel."""
-        return 16 * torch.sigmoid(self.cpb_mlp(self.relative_coords_table).view(-1, self.num_heads))
+        fc1, fc2 = self.cpb_mlp[0], self.cpb_mlp[2]
+        return Fn.CPBBiasFn.apply(self.relative_coords_table, fc1.weight, fc1.bias, fc2.weight)
+
+    def flat_groups(self):
+        """ParamStore adjacency: q_bias, a C-element zero gap, v_bias -> the [3C] qkv bias in place."""
+        return [[self.q_bias, self.dim, self.v_bias]] if self.q_bias is not None else []
 
     def core(self, x2d, dims, ws, shift):
         """x2d [rows, C] -> attention output [rows, C] before proj."""
         C = self.dim
         hd = C // self.num_heads
-        b = torch.cat((self.q_bias, torch.zeros_like(self.v_bias), self.v_bias)) if self.q_bias is not None else None
-        qkv = Fn.linear(x2d, self.qkv.weight, b)
-        scale = torch.clamp(self.logit_scale, max=math.log(1. / 0.01)).exp().view(-1)
-        qkv = Fn.CosineQKFn.apply(qkv, scale, self.num_heads, hd)
+        if self.q_bias is not None:   # qkv bias = cat(q_bias, 0, v_bias) (:151-153): a gapped adjacency group
+            qkv = Fn.linear_group(x2d, (self.qkv.weight,), (self.q_bias, C, self.v_bias))
+        else:
+            qkv = Fn.linear(x2d, self.qkv.weight)
+        qkv = Fn.CosineQKFn.apply(qkv, self.logit_scale, self.num_heads, hd, math.log(1. / 0.01))
         geo = (dims, (1, ws, ws), (1, self.window_size[0], self.window_size[1]), (0, shift, shift),
                self.num_heads, hd, 1.0)
         return Fn.window_attention(qkv, self.bias_table(), None, geo)

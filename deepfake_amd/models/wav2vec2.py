@@ -162,11 +162,15 @@ class Wav2Vec2Attention(nn.Module):
         self.q_proj = nn.Linear(embed_dim, embed_dim)
         self.out_proj = nn.Linear(embed_dim, embed_dim)
 
+    def flat_groups(self):
+        """ParamStore adjacency: q/k/v weights and biases back to back -> one fused qkv GEMM operand."""
+        q, k, v = self.q_proj, self.k_proj, self.v_proj
+        return [[q.weight, k.weight, v.weight], [q.bias, k.bias, v.bias]]
+
     def core(self, x, B, T):
         """x [B*T, C] -> attention output [B*T, C] before out_proj."""
-        w = torch.cat((self.q_proj.weight, self.k_proj.weight, self.v_proj.weight))
-        b = torch.cat((self.q_proj.bias, self.k_proj.bias, self.v_proj.bias))
-        qkv = Fn.linear(x, w, b)
+        q, k, v = self.q_proj, self.k_proj, self.v_proj
+        qkv = Fn.linear_group(x, (q.weight, k.weight, v.weight), (q.bias, k.bias, v.bias))
         geo = ((B, 1, 1, T), (1, 1, T), (1, 1, T), (0, 0, 0), self.num_heads, self.head_dim, self.scaling)
         d = self.dropout.spec() if self.dropout.active(self.training) else None
         return Fn.window_attention(qkv, None, None, geo, drop=d)

@@ -14,7 +14,12 @@ per-parameter zero-fill or AccumulateGrad add (~1600 small kernels per C2 step).
 Parameters reached only through torch ops keep the AccumulateGrad path.
 Parameters are laid out in *reverse* registration order, which is roughly the
 order in which backward produces their gradients (buckets in
-reverse registration order), and each is 16-B aligned.
+reverse registration order), and each is 16-B aligned.  Modules may ask for
+adjacency groups (``flat_groups()``): parameters placed back to back in a given
+order, optionally with zero gaps, so one GEMM reads them as a single operand —
+wav2vec2's q/k/v projections as one [3C, C] weight and [3C] bias, SwinV2's
+(q_bias, 0, v_bias) as the qkv bias — with no per-step concatenation, cast or
+gradient scatter (``group_span``).  Gap elements are never stepped by the SGD.
 """
 import torch
 
@@ -25,14 +30,39 @@ _ALIGN = 8  # elements (bf16 shadow views stay 16-B aligned)
 
 class ParamStore:
     def __init__(self, model, compute_dtype=torch.float32, device=None, direct=True):
-        self.params = [p for p in model.parameters() if p.requires_grad]
-        self.params.reverse()
-        dev = device or self.params[0].device
-        self.offsets = []
+        order = [p for p in model.parameters() if p.requires_grad]
+        order.reverse()
+        dev = device or order[0].device
+        trainable = {id(p) for p in order}
+        group_of = {}
+        for m in model.modules():
+            if hasattr(m, "flat_groups"):
+                for grp in m.flat_groups():
+                    ps = [e for e in grp if not isinstance(e, int)]
+                    sizes = [e if isinstance(e, int) else e.numel() for e in grp]
+                    if all(id(q) in trainable and id(q) not in group_of for q in ps) and \
+                            all(z % _ALIGN == 0 for z in sizes):
+                        for q in ps:
+                            group_of[id(q)] = grp
+        self.params, self.offsets = [], []
+        placed = set()
         n = 0
-        for p in self.params:
-            self.offsets.append(n)
-            n += -(-p.numel() // _ALIGN) * _ALIGN
+        for p in order:
+            grp = group_of.get(id(p))
+            if grp is None:
+                self.params.append(p)
+                self.offsets.append(n)
+                n += -(-p.numel() // _ALIGN) * _ALIGN
+            elif id(grp[0] if not isinstance(grp[0], int) else grp[1]) not in placed:
+                for e in grp:                 # the whole group back to back, in its own order
+                    if isinstance(e, int):
+                        n += e                # zero gap
+                        continue
+                    placed.add(id(e))
+                    self.params.append(e)
+                    self.offsets.append(n)
+                    n += e.numel()
+                placed.add(id(grp[0] if not isinstance(grp[0], int) else grp[1]))
         self.numel = n
         self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
         self.grad = torch.zeros(n, device=dev, dtype=torch.float32)
@@ -87,14 +117,15 @@ class ParamStore:
 
     def touched_runs(self, also=None, every=False):
         """Contiguous [start, end) element ranges of the flat buffers covering the touched
-        parameters (every=True: all parameters), split where ``also[i]`` changes as well."""
+        parameters (every=True: all parameters), split where ``also[i]`` changes and at group gaps."""
         runs = []
         for i, t in enumerate(self.touched):
             if not (t or every):
                 continue
             s, e = self.offsets[i], self.offsets[i] + self.params[i].numel()
             key = also[i] if also is not None else None
-            if runs and runs[-1][2] == key and runs[-1][3] == i - 1:
+            adjacent = runs and s == -(-runs[-1][1] // _ALIGN) * _ALIGN
+            if runs and runs[-1][2] == key and runs[-1][3] == i - 1 and adjacent:
                 runs[-1] = (runs[-1][0], e, key, i)
             else:
                 runs.append((s, e, key, i))
@@ -116,6 +147,29 @@ class ParamStore:
             g = self.grad[o:o + p.numel()].view_as(p)
             if p.grad is None or p.grad.data_ptr() != g.data_ptr():
                 p.grad = g
+
+    def group_span(self, entries):
+        """(start, length) of an adjacency group laid out as given (parameters and int gaps), or None."""
+        first = next(e for e in entries if not isinstance(e, int))
+        i = self.index.get(id(first))
+        if i is None:
+            return None
+        lead = 0
+        for e in entries:
+            if e is first:
+                break
+            lead += e if isinstance(e, int) else e.numel()
+        start = self.offsets[i] - lead
+        o = start
+        for e in entries:
+            if isinstance(e, int):
+                o += e
+                continue
+            j = self.index.get(id(e))
+            if j is None or self.offsets[j] != o:
+                return None
+            o += e.numel()
+        return start, o - start
 
     def span(self, i):
         p, o = self.params[i], self.offsets[i]

@@ -258,12 +258,24 @@ int dfk_w2v_conv0_bwd(const float* wave, int64_t B, int64_t S, const float* w, c
 
 /* SwinV2 cosine-attention prologue (swin_transformer2d.py:154-157) on a [rows, 3C]
  * qkv buffer: q' = normalize(q)*scale[h], k' = normalize(k), v' = v, so the window
- * attention kernel then runs with scale 1 (scale = exp(clamp(logit_scale))).
- * The backward writes dqkv and accumulates dscale[h] (fp32 +=). */
-int dfk_cosine_qk_fwd(const void* qkv, void* out, const float* scale, int64_t rows, int heads, int hd, int dtype,
-                      hipStream_t stream);
-int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, const float* scale, float* dscale,
-                      int64_t rows, int heads, int hd, int dtype, hipStream_t stream);
+ * attention kernel then runs with scale 1; scale[h] = exp(min(logit_scale[h], max_log))
+ * (torch.clamp(logit_scale, max=log(1/0.01)).exp(), :156) from the fp32 parameter itself.
+ * The backward writes dqkv and accumulates the logit_scale gradient dlogit_scale[h] (fp32 +=). */
+int dfk_cosine_qk_fwd(const void* qkv, void* out, const float* logit_scale, float max_log, int64_t rows, int heads,
+                      int hd, int dtype, hipStream_t stream);
+int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, const float* logit_scale, float max_log,
+                      float* dlogit_scale, int64_t rows, int heads, int hd, int dtype, hipStream_t stream);
+
+/* SwinV2 continuous position bias (swin_transformer2d.py:99-100,159-162): out[l][h] =
+ * 16 * sigmoid(sum_j W2[h][j] * relu(W1[j][0]*c[l][0] + W1[j][1]*c[l][1] + b1[j])) for the L = (2Wh-1)(2Ww-1)
+ * relative coordinates c (relative_coords_table), cpb_mlp = Linear(2,hidden) -> ReLU -> Linear(hidden,heads,no
+ * bias); all fp32 (the parameters' own dtype).  bwd: dout [L, heads] -> dW1 [hidden,2], db1 [hidden],
+ * dW2 [heads,hidden] (fp32 +=), recomputing the hidden layer. */
+int dfk_cpb_bias_fwd(const float* coords, const float* w1, const float* b1, const float* w2, float* out, int32_t L,
+                     int32_t hidden, int32_t heads, hipStream_t stream);
+int dfk_cpb_bias_bwd(const float* coords, const float* w1, const float* b1, const float* w2, const float* out,
+                     const float* dout, float* dw1, float* db1, float* dw2, int32_t L, int32_t hidden, int32_t heads,
+                     hipStream_t stream);
 
 /* dx = dy * gelu'(pre) (exact-erf GELU backward, torch nn.GELU / HF ACT2FN["gelu"]). */
 int dfk_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, int dtype, hipStream_t stream);

@@ -108,3 +108,44 @@ def test_layernorm(dt, rows, C):
     K.layernorm_bwd(dy, x, w, mean, rstd, dw2, db2, slab_partials=True)
     assert rel(dw2, wr.grad) < tol(dt)
     assert rel(db2, br.grad) < tol(dt)
+
+
+@pytest.mark.parametrize("heads,clamped", [(4, False), (32, True)])
+def test_cpb_bias_and_cosine_logit_scale(heads, clamped):
+    """SwinV2 16*sigmoid(cpb_mlp(coords)) (swin_transformer2d.py:159-162) and the cosine prologue with
+    exp(clamp(logit_scale, max=log 100)) (:154-157), forward and parameter gradients vs torch fp32."""
+    from deepfake_amd import functional as Fn
+    g = torch.Generator(device=DEV).manual_seed(11)
+    L = 169
+    coords = torch.randn(1, 13, 13, 2, device=DEV, generator=g)
+    mlp = torch.nn.Sequential(torch.nn.Linear(2, 512), torch.nn.ReLU(), torch.nn.Linear(512, heads, bias=False)).to(DEV)
+    ref = 16 * torch.sigmoid(mlp(coords).view(-1, heads))
+    w1, b1, w2 = (p.detach().clone().requires_grad_(True) for p in (mlp[0].weight, mlp[0].bias, mlp[2].weight))
+    out = Fn.CPBBiasFn.apply(coords, w1, b1, w2)
+    assert rel(out, ref) < 1e-5
+    dout = torch.randn(L, heads, device=DEV, generator=g)
+    out.backward(dout)
+    ref.backward(dout)
+    assert rel(w1.grad, mlp[0].weight.grad) < 1e-4
+    assert rel(b1.grad, mlp[0].bias.grad) < 1e-4
+    assert rel(w2.grad, mlp[2].weight.grad) < 1e-4
+    # cosine prologue: q' = normalize(q) * exp(min(logit, log 100)), k' = normalize(k), v' = v
+    rows, hd = 300, 32
+    C = heads * hd
+    qkv = torch.randn(rows, 3 * C, device=DEV, generator=g)
+    logit = (torch.rand(heads, 1, 1, device=DEV, generator=g) * 2 + (4.0 if clamped else 1.0)).requires_grad_(True)
+    x = qkv.clone().requires_grad_(True)
+    y = Fn.CosineQKFn.apply(x, logit, heads, hd, math.log(100.0))
+    xr = qkv.clone().requires_grad_(True)
+    lr = logit.detach().clone().requires_grad_(True)
+    s = torch.clamp(lr, max=math.log(100.0)).exp().view(1, heads, 1)
+    q, k, v = (xr[:, i * C:(i + 1) * C].view(rows, heads, hd) for i in range(3))
+    qn = (torch.nn.functional.normalize(q, dim=-1) * s).reshape(rows, C)
+    kn = torch.nn.functional.normalize(k, dim=-1).reshape(rows, C)
+    yr = torch.cat((qn, kn, v.reshape(rows, C)), 1)
+    assert rel(y, yr) < 1e-5
+    dy = torch.randn(rows, 3 * C, device=DEV, generator=g)
+    y.backward(dy)
+    yr.backward(dy)
+    assert rel(x.grad, xr.grad) < 1e-4
+    assert rel(logit.grad, lr.grad) < 1e-4
