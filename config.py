@@ -9,6 +9,8 @@
                            normalised) or as decoded uint8 RGB frames normalised on the GPU
   --bucket_mb              gradient all-reduce bucket size
   --deterministic          dropout / DropPath / SpecAugment / LayerDrop off (the parity setting, Q12)
+  --video_encoder {swin,inception}   video slot: the north-star Video Swin 3D (default) or the reference's
+                           current InceptionVideoClassifier (Inception-ResNet-v2 + NeXtVLAD, train.py:32,44)
 
 Launch one process per GPU: python -m torch.distributed.run --nproc-per-node N train.py ...
 """
@@ -65,6 +67,7 @@ def build_parser():
     parser.add_argument('--frames', type=str, default='normalized', choices=['normalized', 'uint8'])
     parser.add_argument('--bucket_mb', type=float, default=64.0)
     parser.add_argument('--deterministic', action='store_true')
+    parser.add_argument('--video_encoder', type=str, default='swin', choices=['swin', 'inception'])
     return parser
 
 

@@ -34,7 +34,8 @@ class GemmArgs(C.Structure):
                 ("M", C.c_int32), ("N", C.c_int32), ("K", C.c_int32), ("dtype", C.c_int32),
                 ("a_kmajor", C.c_int32), ("b_kmajor", C.c_int32), ("c_f32", C.c_int32), ("nz0", C.c_int32),
                 ("nz1", C.c_int32), ("splitk", C.c_int32), ("act", C.c_int32), ("atomic", C.c_int32),
-                ("beta", C.c_float), ("ws", C.c_void_p), ("rowsum", C.c_void_p), ("drop", Drop)]
+                ("beta", C.c_float), ("ws", C.c_void_p), ("rowsum", C.c_void_p), ("drop", Drop),
+                ("alpha", C.c_float)]
 
 
 class WattnArgs(C.Structure):
@@ -62,6 +63,12 @@ class PatchEmbedArgs(C.Structure):
                 ("C", C.c_int32), ("w", C.c_void_p), ("b", C.c_void_p), ("ln_w", C.c_void_p), ("ln_b", C.c_void_p),
                 ("eps", C.c_float), ("out", C.c_void_p), ("mean", C.c_void_p), ("rstd", C.c_void_p),
                 ("dw", C.c_void_p), ("db", C.c_void_p), ("dln_w", C.c_void_p), ("dln_b", C.c_void_p)]
+
+
+class Conv2dGeo(C.Structure):
+    _fields_ = [("N", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("C", C.c_int32), ("kh", C.c_int32),
+                ("kw", C.c_int32), ("sh", C.c_int32), ("sw", C.c_int32), ("ph", C.c_int32), ("pw", C.c_int32),
+                ("Ho", C.c_int32), ("Wo", C.c_int32)]
 
 
 class Im2colArgs(C.Structure):
@@ -98,6 +105,15 @@ SIGNATURES = {
     "dfk_w2v_conv0_fwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP],
     "dfk_w2v_conv0_bwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _VP, _VP, _VP, _VP],
     "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP, _VP],
+    "dfk_im2col2d": [_VP, _I64, _VP, C.POINTER(Conv2dGeo), C.c_int, _VP],
+    "dfk_col2im2d": [_VP, _VP, _I64, C.POINTER(Conv2dGeo), C.c_int, C.c_int, _VP],
+    "dfk_bn2d_fwd": [_VP, _I64, _VP, _I64, _I64, _I32, _VP, _VP, _F, _F, C.c_int, _VP, _VP, _VP, _VP, _VP, C.c_int,
+                     _VP],
+    "dfk_bn2d_apply": [_VP, _I64, _VP, _I64, _I64, _I32, _VP, _VP, _VP, _VP, C.c_int, C.c_int, _VP],
+    "dfk_bn2d_bwd": [_VP, _I64, _VP, _I64, _VP, _I64, _VP, _I64, _I64, _I32, _VP, _VP, _VP, C.c_int, _VP, _VP, _VP,
+                     C.c_int, _VP],
+    "dfk_pool2d_fwd": [_VP, _I64, _VP, _I64, C.POINTER(Conv2dGeo), C.c_int, C.c_int, _VP],
+    "dfk_pool2d_bwd": [_VP, _I64, _VP, _I64, _VP, _I64, C.POINTER(Conv2dGeo), C.c_int, C.c_int, C.c_int, _VP],
     "dfk_dropout": [_VP, _VP, _I64, _I32, _I64, C.POINTER(Drop), C.c_int, _VP],
     "dfk_bernoulli_flags": [C.POINTER(Drop), _I32, _VP, _VP],
     "dfk_spec_augment_fwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _F, _I32, _I32, C.POINTER(Drop), C.c_int, _VP],

@@ -185,11 +185,15 @@ __device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1
       for (int e = 0; e < 8; ++e) v[e] *= drop_mul(dc, rr, col0 + e);
     }
   }
+  if (g.alpha != 0.f && g.alpha != 1.f)   // Inception residual scale (0 reads as 1)
+    for (int e = 0; e < 8; ++e) v[e] *= g.alpha;
   if (res) {
     const T* rp = res + (long)row * g.ldr + col0;
     if (full) { float r8[8]; ld8<T>(rp, r8); for (int e = 0; e < 8; ++e) v[e] += r8[e]; }
     else for (int e = 0; e < ncol; ++e) v[e] += ldf<T>(rp + e);
   }
+  if (g.act == 3)   // ReLU after the residual add
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
   const long ci = coff + (long)row * g.ldc + col0;
   if (g.atomic) {
     float* C = reinterpret_cast<float*>(g.c) + ci;
@@ -501,7 +505,8 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   if (g.splitk < 1 || g.nz0 < 1 || g.nz1 < 1) return DFK_EINVAL;
   if (g.splitk > 1 && !g.atomic && !g.ws) return DFK_EINVAL;   // explicit split-K: fp32 slabs in ws
   if (g.atomic && (!g.c_f32 || g.bias || g.residual || g.act)) return DFK_EINVAL;
-  if (g.act && g.act != 1 && !g.aux) return DFK_EINVAL;
+  if (g.act == 2 && !g.aux) return DFK_EINVAL;
+  if (g.act < 0 || g.act > 3 || (g.act == 3 && (g.c_f32 || g.atomic))) return DFK_EINVAL;
   if (g.rowsum && (g.nz0 != 1 || g.nz1 != 1 || !g.a_kmajor || !g.b_kmajor)) return DFK_EINVAL;
   if (g.drop.mode && (g.c_f32 || g.atomic || !g.drop.rng || !(g.drop.p >= 0.f && g.drop.p < 1.f))) return DFK_EINVAL;
   if (g.M <= 0 || g.N <= 0) return 0;

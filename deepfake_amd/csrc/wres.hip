@@ -237,7 +237,7 @@ int dfk_wres_try(const dfk_gemm_args& g, hipStream_t s) {
   if (g.dtype != DFK_BF16 || g.a_kmajor || g.c_f32 || g.atomic || g.splitk != 1 || g.rowsum) return 0;
   if (g.nz0 != 1 || g.nz1 != 1 || g.a.conv_cg > 0 || g.b.conv_cg > 0 || g.beta != 0.f) return 0;
   if (g.M < 16384 || g.K % 32 || g.K > 384 || g.N % 4) return 0;
-  if (g.act == 2 && !g.aux) return 0;
+  if ((g.act == 2 && !g.aux) || g.act == 3 || (g.alpha != 0.f && g.alpha != 1.f)) return 0;
   if (g.a.ld % 8 || ((uintptr_t)g.a.ptr & 15) || g.b.ld % 8 || ((uintptr_t)g.b.ptr & 15)) return 0;
   if (g.ldc % 4 || !al8(g.c) || (g.bias && !al8(g.bias)) || (g.residual && (g.ldr % 4 || !al8(g.residual))) ||
       (g.aux && (g.ldaux % 4 || !al8(g.aux))))

@@ -10,10 +10,21 @@ import torch
 from . import kernels as K
 
 
+def _orig(p):
+    """The ParamStore parameter behind p: p itself, or — for the detached alias an activation-checkpoint
+    recompute hands back from ctx.saved_tensors — the parameter with the same storage (params.PARAM_BY_PTR)."""
+    if p is None or hasattr(p, "_dfk_store") or not isinstance(p, torch.Tensor):
+        return p
+    from .params import PARAM_BY_PTR
+    q = PARAM_BY_PTR.get(p.data_ptr())
+    return q if q is not None and q.shape == p.shape else p
+
+
 def compute_weight(p, dtype):
     """Weight in the compute dtype: the parameter itself (fp32) or its bf16 shadow."""
     if p is None:
         return None
+    p = _orig(p)
     if p.dtype == dtype:
         return p
     sh = getattr(p, "_dfk_shadow", None)
@@ -27,14 +38,18 @@ def _f32_zeros(p):
 
 
 def _store(p):
-    return getattr(p, "_dfk_store", None) if p is not None else None
+    return getattr(_orig(p), "_dfk_store", None) if p is not None else None
+
+
+_RECOMPUTING = [0]   # > 0 inside an activation-checkpoint recompute (the use was counted in the first forward)
 
 
 def grad_use(ctx, idx, p):
     """Forward side of a direct-gradient parameter: count this use so that the
     last backward contribution (grad_done) is the one that reports p ready."""
+    p = _orig(p)
     st = _store(p)
-    if st is not None and ctx.needs_input_grad[idx]:
+    if st is not None and ctx.needs_input_grad[idx] and not _RECOMPUTING[0]:
         st.uses[id(p)] = st.uses.get(id(p), 0) + 1
 
 
@@ -43,6 +58,7 @@ def grad_sink(p):
     With a ParamStore in direct mode this is p.grad itself (a view of the flat
     gradient buffer, zeroed once per step): the kernels' fp32 atomics add
     straight into it and autograd never runs a fill or AccumulateGrad add for p."""
+    p = _orig(p)
     st = _store(p)
     if st is not None:
         if p.grad is None:
@@ -54,11 +70,32 @@ def grad_sink(p):
 def grad_done(p, g):
     """Value to return to autograd for p, after its kernels accumulated into g
     (None in direct mode: the gradient is already in p.grad)."""
+    p = _orig(p)
     st = _store(p)
     if st is None:
         return g
     st.grad_ready(p)
     return None
+
+
+def checkpoint(fn, *args):
+    """torch.utils.checkpoint (non-reentrant) of a region of HIP ops — the reference's use_checkpoint
+    (video_swin_transformer.py:267-276, swin_transformer2d.py:428-429): the region's activations are dropped
+    after the forward and recomputed in the backward.  The recompute is marked so direct-gradient use
+    counts stay one per forward use, and the counter-based dropout masks (deepfake_amd.rng) redraw exactly
+    the forward's masks (same seed, step and site)."""
+    import contextlib
+    import torch.utils.checkpoint as cp
+
+    @contextlib.contextmanager
+    def recompute():
+        _RECOMPUTING[0] += 1
+        try:
+            yield
+        finally:
+            _RECOMPUTING[0] -= 1
+    return cp.checkpoint(fn, *args, use_reentrant=False,
+                         context_fn=lambda: (contextlib.nullcontext(), recompute()))
 
 
 def rows2d(x):
@@ -582,3 +619,120 @@ class PatchEmbedFn(torch.autograd.Function):
         dw, db = grad_sink(weight), grad_sink(bias)
         K.linear_dw(dy, cols, dw.view(weight.shape[0], -1), db=db)
         return None, grad_done(weight, dw), grad_done(bias, db), None, None, None
+
+
+# ---------------------------------------------------------------- 2-D convolution family (SURVEY §8f f4)
+def _conv_weight2d(weight, dt):
+    """[Cout, Cin, kh, kw] -> the GEMM operand [Cout, kh*kw*Cin] (tap-major, channel-fastest: im2col's columns)."""
+    w = compute_weight(weight, dt)
+    if w.shape[2] == 1 and w.shape[3] == 1:
+        return w.reshape(w.shape[0], w.shape[1])
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()
+
+
+class ConvBNReLUFn(torch.autograd.Function):
+    """The reference's Conv2d block (InceptionResV2.py:6-16): nn.Conv2d(bias=False) -> BatchNorm2d(eps 1e-3,
+    momentum 0.1) -> ReLU on channels-last [N, H, W, C] activations.  k x k / strided convs run as im2col +
+    MFMA GEMM, 1x1 stride-1 convs as the GEMM on the activation rows; training-mode BN uses batch statistics and
+    updates the running ones (eval mode: the running ones)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, bn, k, s, p, training):
+        N, H, W, C = x.shape
+        dt = x.dtype
+        g = K.conv2d_geo(N, H, W, C, k, s, p)
+        w2 = _conv_weight2d(weight, dt)
+        Cout = w2.shape[0]
+        one = g.kh == 1 and g.kw == 1 and g.sh == 1 and g.sw == 1 and g.ph == 0 and g.pw == 0
+        cols = x.reshape(N * H * W, C) if one and x.is_contiguous() else K.im2col2d(x, g)
+        z = K.linear(cols, w2)
+        y = torch.empty_like(z)
+        gm, bt = gamma.detach().float(), beta.detach().float()
+        if training:
+            mean, rstd = K.bn2d_fwd(z, y, gm, bt, bn.eps, bn.momentum, True, bn.running_mean, bn.running_var)
+        else:
+            mean = bn.running_mean.float()
+            rstd = torch.rsqrt(bn.running_var.float() + bn.eps)
+            K.bn2d_apply(z, y, mean, rstd, gm, bt, True)
+        for i, q in ((1, weight), (2, gamma), (3, beta)):
+            grad_use(ctx, i, q)
+        ctx.save_for_backward(cols, w2, z, y, mean, rstd, weight, gamma, beta)
+        ctx.g, ctx.one, ctx.xshape = g, one, x.shape
+        return y.view(N, g.Ho, g.Wo, Cout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, w2, z, y, mean, rstd, weight, gamma, beta = ctx.saved_tensors
+        g = ctx.g
+        dy2 = dy.reshape(z.shape).contiguous()
+        dz = torch.empty_like(z)
+        dg, db = grad_sink(gamma), grad_sink(beta)
+        K.bn2d_bwd(dy2, y, z, dz, mean, rstd, gamma.detach().float(), True, dg, db)
+        dw = grad_sink(weight)
+        kh, kw = g.kh, g.kw
+        if kh == 1 and kw == 1:
+            K.linear_dw(dz, cols, dw.view(dw.shape[0], -1))
+        else:
+            dw2 = torch.zeros(w2.shape, device=dz.device, dtype=torch.float32)
+            K.linear_dw(dz, cols, dw2)
+            dw += dw2.view(dw.shape[0], kh, kw, -1).permute(0, 3, 1, 2)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dcols = K.linear_dx(dz, w2)
+            if ctx.one:
+                dx = dcols.view(ctx.xshape)
+            else:
+                dx = torch.empty(ctx.xshape, device=dz.device, dtype=dz.dtype)
+                K.col2im2d(dcols, g, dx)
+        return dx, grad_done(weight, dw), grad_done(gamma, dg), grad_done(beta, db), None, None, None, None, None
+
+
+class ResConvFn(torch.autograd.Function):
+    """Inception-ResNet residual (InceptionResV2.py:90-95,112-117,159-166): y = relu?(x + scale * conv1x1(x_res)),
+    the conv with bias, as one GEMM with the scale / residual / ReLU epilogue."""
+
+    @staticmethod
+    def forward(ctx, xres, weight, bias, x, scale, relu):
+        N, H, W, C = x.shape
+        dt = x.dtype
+        w2 = _conv_weight2d(weight, dt)
+        a = xres.reshape(-1, xres.shape[-1])
+        y = torch.empty(N * H * W, C, device=x.device, dtype=dt)
+        K.gemm(a, a.stride(0), False, w2, w2.stride(0), False, a.shape[0], C, a.shape[1], y, C, dtype=K.L.dt(x),
+               bias=compute_weight(bias, dt), residual=x.reshape(-1, C), ldr=C, act=3 if relu else 0,
+               alpha=float(scale))
+        for i, q in ((1, weight), (2, bias)):
+            grad_use(ctx, i, q)
+        ctx.save_for_backward(a, w2, y, weight, bias)
+        ctx.scale, ctx.relu, ctx.xres_shape = float(scale), relu, xres.shape
+        return y.view(N, H, W, C)
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, w2, y, weight, bias = ctx.saved_tensors
+        dy2 = dy.reshape(y.shape)
+        if ctx.relu:
+            dy2 = dy2 * (y > 0).to(dy2.dtype)
+        dy2 = dy2.contiguous()
+        dz = (dy2 * ctx.scale).contiguous()
+        dw, db = grad_sink(weight), grad_sink(bias)
+        K.linear_dw(dz, a, dw.view(dw.shape[0], -1), db=db)
+        dxres = K.linear_dx(dz, w2).view(ctx.xres_shape)
+        return dxres, grad_done(weight, dw), grad_done(bias, db), dy2.view(dy.shape), None, None
+
+
+class Pool2dFn(torch.autograd.Function):
+    """MaxPool2d(3, s, 0) (mode 0) / AvgPool2d(3, 1, 1, count_include_pad=False) (mode 1) on [N, H, W, C]."""
+
+    @staticmethod
+    def forward(ctx, x, k, s, p, mode):
+        N, H, W, C = x.shape
+        g = K.conv2d_geo(N, H, W, C, k, s, p)
+        ctx.save_for_backward(x)
+        ctx.g, ctx.mode = g, mode
+        return K.pool2d_fwd(x, g, mode)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, = ctx.saved_tensors
+        return K.pool2d_bwd(x, dy.contiguous(), ctx.g, ctx.mode), None, None, None, None

@@ -26,7 +26,7 @@ def _view(t, ld, bs0=0, bs1=0, conv=None):
 def gemm(a, a_ld, a_kmajor, b, b_ld, b_kmajor, M, N, K, c, ldc, *, dtype, c_f32=False, bias=None,
          residual=None, ldr=0, aux=None, ldaux=0, act=0, beta=0.0, atomic=False, splitk=1,
          nz=(1, 1), a_bs=(0, 0), b_bs=(0, 0), c_bs=(0, 0), r_bs=(0, 0), a_conv=None, b_conv=None, bias_bs1=0,
-         rowsum=None, drop=None):
+         rowsum=None, drop=None, alpha=0.0):
     """Raw dfk_gemm.  a/b/c are tensors (base pointers); see include/dfk.h.  drop: rng.Drop spec of the
     output's dropout / DropPath (applied before the residual add)."""
     g = L.GemmArgs()
@@ -52,6 +52,7 @@ def gemm(a, a_ld, a_kmajor, b, b_ld, b_kmajor, M, N, K, c, ldc, *, dtype, c_f32=
     g.atomic = int(atomic)
     g.beta = float(beta)
     g.rowsum = rowsum.data_ptr() if rowsum is not None else None
+    g.alpha = float(alpha)
     for t in (a, b, c):
         if not t.is_cuda:
             raise RuntimeError("deepfake_amd: tensors must be on the HIP device (no CPU fallback)")
@@ -407,4 +408,70 @@ def spec_augment_bwd(dy, mask, dembed):
     dx = torch.empty_like(dy)
     L.check(L.lib().dfk_spec_augment_bwd(L.ptr(dy), L.ptr(dx), L.ptr(mask), L.ptr(dembed), B, T, C, L.dt(dy),
                                          L.stream()), "spec_augment_bwd")
+    return dx
+
+
+def conv2d_geo(N, H, W, C, k, s, p):
+    """dfk_conv2d_geo for a (kh, kw) kernel with stride s and padding p (ints or pairs)."""
+    kh, kw = (k, k) if isinstance(k, int) else k
+    sh, sw = (s, s) if isinstance(s, int) else s
+    ph, pw = (p, p) if isinstance(p, int) else p
+    g = L.Conv2dGeo()
+    g.N, g.H, g.W, g.C, g.kh, g.kw, g.sh, g.sw, g.ph, g.pw = N, H, W, C, kh, kw, sh, sw, ph, pw
+    g.Ho, g.Wo = (H + 2 * ph - kh) // sh + 1, (W + 2 * pw - kw) // sw + 1
+    return g
+
+
+def im2col2d(x, g):
+    """x: NHWC view [N, H, W, C] (pixel stride x.stride(2)) -> [N*Ho*Wo, kh*kw*C]."""
+    out = torch.empty(g.N * g.Ho * g.Wo, g.kh * g.kw * g.C, device=x.device, dtype=x.dtype)
+    L.check(L.lib().dfk_im2col2d(L.ptr(x), x.stride(2), L.ptr(out), g, L.dt(x), L.stream()), "im2col2d")
+    return out
+
+
+def col2im2d(dcols, g, dx, accumulate=False):
+    L.check(L.lib().dfk_col2im2d(L.ptr(dcols), L.ptr(dx), dx.stride(2), g, int(accumulate), L.dt(dcols), L.stream()),
+            "col2im2d")
+    return dx
+
+
+def bn2d_fwd(x2, y2, gamma, beta, eps, momentum, relu, running_mean=None, running_var=None):
+    """Training-mode BatchNorm over the rows of 2-D views x2 -> y2 (+ReLU); returns (mean, rstd)."""
+    rows, C = x2.shape
+    mean = torch.empty(C, device=x2.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    ws = torch.empty(2 * C, device=x2.device, dtype=torch.float32)
+    L.check(L.lib().dfk_bn2d_fwd(L.ptr(x2), x2.stride(0), L.ptr(y2), y2.stride(0), rows, C, L.ptr(gamma), L.ptr(beta),
+                                 float(eps), float(momentum), int(relu), L.ptr(mean), L.ptr(rstd),
+                                 L.ptr(running_mean), L.ptr(running_var), L.ptr(ws), L.dt(x2), L.stream()), "bn2d_fwd")
+    return mean, rstd
+
+
+def bn2d_apply(x2, y2, mean, rstd, gamma, beta, relu):
+    rows, C = x2.shape
+    L.check(L.lib().dfk_bn2d_apply(L.ptr(x2), x2.stride(0), L.ptr(y2), y2.stride(0), rows, C, L.ptr(mean), L.ptr(rstd),
+                                   L.ptr(gamma), L.ptr(beta), int(relu), L.dt(x2), L.stream()), "bn2d_apply")
+
+
+def bn2d_bwd(dy2, y2, x2, dx2, mean, rstd, gamma, relu, dgamma, dbeta):
+    rows, C = x2.shape
+    ws = torch.empty(2 * C, device=x2.device, dtype=torch.float32)
+    L.check(L.lib().dfk_bn2d_bwd(L.ptr(dy2), dy2.stride(0), L.ptr(y2), y2.stride(0) if y2 is not None else 0,
+                                 L.ptr(x2), x2.stride(0), L.ptr(dx2), dx2.stride(0), rows, C, L.ptr(mean), L.ptr(rstd),
+                                 L.ptr(gamma), int(relu), L.ptr(dgamma), L.ptr(dbeta), L.ptr(ws), L.dt(x2),
+                                 L.stream()), "bn2d_bwd")
+
+
+def pool2d_fwd(x, g, mode):
+    y = torch.empty(g.N, g.Ho, g.Wo, g.C, device=x.device, dtype=x.dtype)
+    L.check(L.lib().dfk_pool2d_fwd(L.ptr(x), x.stride(2), L.ptr(y), y.stride(2), g, int(mode), L.dt(x), L.stream()),
+            "pool2d_fwd")
+    return y
+
+
+def pool2d_bwd(x, dy, g, mode, dx=None):
+    if dx is None:
+        dx = torch.empty(g.N, g.H, g.W, g.C, device=x.device, dtype=x.dtype)
+    L.check(L.lib().dfk_pool2d_bwd(L.ptr(x), x.stride(2), L.ptr(dy), dy.stride(2), L.ptr(dx), dx.stride(2), g,
+                                   int(mode), 0, L.dt(x), L.stream()), "pool2d_bwd")
     return dx

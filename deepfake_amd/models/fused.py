@@ -40,7 +40,7 @@ CONFIGS = {
                seconds=4, B=8),
     "c4": dict(vst=_VST_B, mel=_MEL_C2, w2v_layers=12, video_dim=1024, audio_dim=1024, T=32, H=224, W=224,
                seconds=4, B=8),
-    "c5": dict(vst=_VST_T, mel=_MEL_C2, w2v_layers=12, video_dim=768, audio_dim=1024, T=64, H=224, W=224,
+    "c5": dict(vst=dict(_VST_T, use_checkpoint=True), mel=_MEL_C2, w2v_layers=12, video_dim=768, audio_dim=1024, T=64, H=224, W=224,
                seconds=10, B=8),
 }
 
@@ -79,6 +79,17 @@ def build_model(args, compute_dtype=torch.float32):
     from .video_swin_transformer import VideoClassifier
     cfg = CONFIGS[getattr(args, "config", "c2")]
     reg = not getattr(args, "deterministic", False)
+    if getattr(args, "video_encoder", "swin") == "inception":   # the reference's current video branch
+        from .IResNet import InceptionVideoClassifier
+        drop = args.swin_drop if reg else 0.0
+        if args.modality == "video":          # train.py:32
+            return set_compute_dtype(InceptionVideoClassifier(args, 1, drop_rate=drop), compute_dtype)
+        if args.modality == "fused":          # train.py:42-46: video_dim = hidden_size 1024
+            m = build_fused(cfg, args, compute_dtype=compute_dtype, regularize=reg)
+            ve = InceptionVideoClassifier(args, 1, drop_rate=drop, use_feat=True)
+            m.vExtract = ve
+            m.video_projection = torch.nn.Linear(1024, m.video_projection.out_features)
+            return set_compute_dtype(m, compute_dtype)
     if args.modality == "fused":
         return build_fused(cfg, args, compute_dtype=compute_dtype, regularize=reg)
     if args.modality == "video":

@@ -202,7 +202,10 @@ class BasicLayer(nn.Module):
 
     def forward(self, x):
         for blk in self.blocks:
-            x = blk(x)
+            if self.use_checkpoint and self.training and torch.is_grad_enabled():   # :428-429
+                x = Fn.checkpoint(blk, x)
+            else:
+                x = blk(x)
         return self.downsample(x) if self.downsample is not None else x
 
     def _init_respostnorm(self):

@@ -144,15 +144,26 @@ class SwinTransformerBlock3D(nn.Module):
         qkv = Fn.linear(xn.reshape(-1, C), self.attn.qkv.weight, self.attn.qkv.bias)
         return self.attn.core(qkv, (B, D, H, W), ws, ss)
 
+    def _attn_branch(self, x, dp):
+        """x + DropPath(proj(W-MSA(LN1 x)))  (forward_part1 + the first residual, :266-271)."""
+        B, D, H, W, C = x.shape
+        o = self.forward_part1(x)
+        return Fn.linear(o, self.attn.proj.weight, self.attn.proj.bias, residual=x.reshape(-1, C),
+                         drop=dp).view(B, D, H, W, C)
+
+    def _mlp_branch(self, x, dp):
+        """x + DropPath(mlp(LN2 x))  (forward_part2 + the second residual, :273-276)."""
+        return Fn.mlp(Fn.layer_norm(x, self.norm2), self.mlp.fc1, self.mlp.fc2, residual=x, drop_out=dp)
+
     def forward(self, x, mask_matrix=None):
         B, D, H, W, C = x.shape
         on = self.dp is not None and self.training
         dp = (self.dp[0].spec(D * H * W), self.dp[1].spec(D * H * W)) if on else (None, None)
-        o = self.forward_part1(x, mask_matrix)
-        x = Fn.linear(o, self.attn.proj.weight, self.attn.proj.bias, residual=x.reshape(-1, C),
-                      drop=dp[0])                                                    # x + DropPath(proj(o))
-        x = Fn.mlp(Fn.layer_norm(x, self.norm2), self.mlp.fc1, self.mlp.fc2, residual=x,
-                   drop_out=dp[1])                                                      # x + DropPath(mlp(LN2 x))
+        if self.use_checkpoint and self.training and torch.is_grad_enabled():   # :267-276
+            x = Fn.checkpoint(self._attn_branch, x, dp[0])
+            x = Fn.checkpoint(self._mlp_branch, x, dp[1])
+        else:
+            x = self._mlp_branch(self._attn_branch(x, dp[0]), dp[1])
         return x.view(B, D, H, W, C)
 
 

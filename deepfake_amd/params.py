@@ -26,6 +26,7 @@ import torch
 from . import kernels as K
 
 _ALIGN = 8  # elements (bf16 shadow views stay 16-B aligned)
+PARAM_BY_PTR = {}   # flat-buffer address -> parameter (resolves aliases handed back by checkpoint recomputes)
 
 
 class ParamStore:
@@ -77,6 +78,7 @@ class ParamStore:
                     p._dfk_shadow = self.shadow[o:o + p.numel()].view_as(p)
                 if direct:
                     p._dfk_store = self
+                    PARAM_BY_PTR[p.data_ptr()] = p
         self.index = {id(p): i for i, p in enumerate(self.params)}
         self.uses = {}           # id(p) -> forward uses whose backward has not run yet (direct mode)
         self.listeners = []      # callbacks(i) when parameter i's gradient is complete

@@ -69,7 +69,9 @@ typedef struct {
  *   :291 (PatchMerging.reduction), ModalFusion.py:16-25, HF modeling_wav2vec2.py
  *   :258-272 (conv1..6), :326-368 (pos-conv), :495-498,:556-561 (encoder linears).
  * Epilogue, in order: +bias[j]; act==1: aux<-v (if aux), v=gelu(v);
- *   act==2: v *= gelu'(aux[i,j]); v *= drop mask (row i + z*M, col j); +residual[i,j]; then store
+ *   act==2: v *= gelu'(aux[i,j]); v *= drop mask (row i + z*M, col j); v *= alpha (0 reads as 1);
+ *   +residual[i,j]; act==3: v = relu(v) (Inception-ResNet blocks: relu(x + scale*conv(x_res)),
+ *   InceptionResV2.py:95,117,164); then store
  *   (beta: v += beta*C_old) or fp32 atomicAdd (atomic=1, for split-K / batch-summed weight grads).
  * Contract: the contiguous extent and ld of each view are multiples of 8 (bf16) / 4 (f32). */
 typedef struct {
@@ -96,6 +98,7 @@ typedef struct {
   float* rowsum;        /* optional, nz0 = nz1 = 1: rowsum[i] += sum_k A(i,k) (fp32) — the bias gradient
                            of a Linear when A = dy^T, computed by one extra MFMA against a ones operand */
   dfk_drop drop;        /* dropout / DropPath of the output before the residual add (bf16/f32 C only) */
+  float alpha;          /* scale of the product (+bias) before the residual add; 0 = 1 */
 } dfk_gemm_args;
 int dfk_gemm(const dfk_gemm_args* g, hipStream_t stream);
 /* Bytes of scratch dfk_gemm wants in g->ws: grids too small to fill the chip (the
@@ -319,6 +322,40 @@ int dfk_frame_normalize(const uint8_t* src, float* dst, int64_t frames, int32_t 
  * (transformers feature_extraction_wav2vec2.py:94-95, called at src/trainer.py:258) of every row of a
  * zero-padded [B, S] batch (no attention mask, Q13): y = (x - mean) / sqrt(var + eps), eps = 1e-7. */
 int dfk_wave_normalize(const float* x, float* y, int64_t B, int64_t S, float eps, hipStream_t stream);
+
+/* ---- 2-D convolution family of the Inception-ResNet-v2 video branch (SURVEY.md §8f f4:
+ * src/models/InceptionResV2.py:6-190, IResNet.py:331-393).  Activations are channels-last [N*H*W, C] rows with
+ * a row stride ld (>= C), so a branch reads / writes a channel slice of a torch.cat buffer in place. */
+typedef struct {
+  int32_t N, H, W, C;       /* input */
+  int32_t kh, kw, sh, sw, ph, pw;
+  int32_t Ho, Wo;           /* output */
+} dfk_conv2d_geo;
+/* im2col of nn.Conv2d (InceptionResV2.py:9): out [N*Ho*Wo][(ky*kw + kx)*C + c] (zero padding); the conv is
+ * then the GEMM out . W'^T with W' = weight.permute(0,2,3,1) [Cout][kh*kw*C].  col2im2d: the input gradient
+ * dx (=, or += when accumulate) from dcols of the same layout (a gather: no atomics). */
+int dfk_im2col2d(const void* x, int64_t ldx, void* out, const dfk_conv2d_geo* g, int dtype, hipStream_t stream);
+int dfk_col2im2d(const void* dcols, void* dx, int64_t ldx, const dfk_conv2d_geo* g, int accumulate, int dtype,
+                 hipStream_t stream);
+/* BatchNorm2d in training mode (+ the ReLU of the reference's Conv2d block, InceptionResV2.py:10-15): batch
+ * statistics per channel over all rows (fp32), running_mean / running_var updated with momentum (unbiased
+ * variance; may both be NULL); mean / rstd [C] saved for the backward; ws [2C] fp32 scratch.
+ * bn2d_apply: y = (x - mean) * rstd * gamma + beta (+ReLU) from given statistics (eval mode: the running ones). */
+int dfk_bn2d_fwd(const void* x, int64_t ldx, void* y, int64_t ldy, int64_t rows, int32_t C, const float* gamma,
+                 const float* beta, float eps, float momentum, int relu, float* mean, float* rstd,
+                 float* running_mean, float* running_var, float* ws, int dtype, hipStream_t stream);
+int dfk_bn2d_apply(const void* x, int64_t ldx, void* y, int64_t ldy, int64_t rows, int32_t C, const float* mean,
+                   const float* rstd, const float* gamma, const float* beta, int relu, int dtype, hipStream_t stream);
+/* backward of y = relu?(BN(x)): dx (=), dgamma / dbeta (fp32 +=, may be NULL); y is read for the ReLU mask. */
+int dfk_bn2d_bwd(const void* dy, int64_t lddy, const void* y, int64_t ldy, const void* x, int64_t ldx, void* dx,
+                 int64_t lddx, int64_t rows, int32_t C, const float* mean, const float* rstd, const float* gamma,
+                 int relu, float* dgamma, float* dbeta, float* ws, int dtype, hipStream_t stream);
+/* MaxPool2d(k, s, p) (mode 0; backward routes to the first maximum of each window, as torch) and AvgPool2d(k, s, p,
+ * count_include_pad=False) (mode 1): InceptionResV2.py:27,43,47,61,122.  bwd: dx (=, or += when accumulate). */
+int dfk_pool2d_fwd(const void* x, int64_t ldx, void* y, int64_t ldy, const dfk_conv2d_geo* g, int mode, int dtype,
+                   hipStream_t stream);
+int dfk_pool2d_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx,
+                   const dfk_conv2d_geo* g, int mode, int accumulate, int dtype, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -82,6 +82,14 @@ FUSED_C2 = dict(
              window_size=7, drop_path_rate=0.0, pretrained_window_sizes=(16, 16, 16, 16)),
     w2v_layers=12, video_dim=768, audio_dim=1024)
 
+# the reference's Inception-ResNet-v2 + NeXtVLAD video branch, smallest viable frame size
+INCEPTION = dict(name="inception_b2t2", seed=191, B=2, T=2, HW=75, sample=256,
+                 bn_keys=("inceptionRes.features.0.features.0.bn.running_mean",
+                          "inceptionRes.features.0.features.0.bn.running_var",
+                          "inceptionRes.features.5.branch_1.1.bn.running_var",
+                          "inceptionRes.conv.bn.running_mean", "video_nextvlad.bn0.running_mean",
+                          "video_nextvlad.bn1.running_var", "bn0.running_mean", "bn1.running_var"))
+
 GRAD_SAMPLE_C1 = 1024   # per-parameter gradient tensors of the fused train steps: strided samples + norm
 GRAD_SAMPLE_C2 = 512
 

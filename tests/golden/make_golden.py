@@ -340,10 +340,42 @@ def case_config_flags():
     print("config flags:", len(flags))
 
 
+def case_inception():
+    """the reference's InceptionVideoClassifier (IResNet.py:331-393 over InceptionResV2.py) at a
+    small frame size (B=2 clips x T=2 frames x 75x75 — the smallest input the stem/reductions accept), training
+    mode (batch-statistics BatchNorm), drop_rate 0 and classify_drop 0 (the reference's F.dropout calls are
+    always on, so dropout is off for a deterministic fixture): probabilities, BCE loss, gradients (sampled),
+    BatchNorm running statistics after the step, the eval-mode probabilities that follow, and the state_dict
+    keys / shapes."""
+    import json
+    import src.models.IResNet as IR
+    c = GC.INCEPTION
+    args = types.SimpleNamespace(bn_momentum=0.1, num_frames=c["T"], classify_drop=0.0)
+    m = IR.InceptionVideoClassifier(args, num_classes=1, drop_rate=0.0)
+    named_fill_(m, seed=c["seed"])
+    x = randn(c["seed"] + 1, (c["B"], c["T"], 3, c["HW"], c["HW"]))
+    label = torch.tensor([1.0, 0.0])
+    m.train()
+    prob = m(x)
+    loss = torch.nn.BCELoss()(prob, label)
+    loss.backward()
+    out = dict(prob=prob.detach(), loss=loss.detach())   # x is re-drawn by oracle.fill.randn(seed + 1, shape)
+    out.update({k: v for k, v in grads_of(m).items()})
+    sd = m.state_dict()
+    for k in c["bn_keys"]:
+        out["s:" + k] = sd[k]
+    m.eval()
+    with torch.no_grad():
+        out["prob_eval"] = m(x)
+    save(c["name"], _big=c["sample"], _sample=c["sample"], **out)
+    with open(os.path.join(HERE, "inception_keys.json"), "w") as f:
+        json.dump([[k, list(v.shape)] for k, v in sd.items()], f)
+
+
 if __name__ == "__main__":
     only = sys.argv[1:]
     for fn in [case_window_attention, case_block, case_patch_embed_merge, case_vst_c1, case_w2v, case_head,
                case_fused_c1, case_block_c2, case_mel_c2, case_fused_c1_grads, case_fused_c2, case_state_keys,
-               case_config_flags]:
+               case_config_flags, case_inception]:
         if not only or fn.__name__ in only:
             fn()

@@ -36,6 +36,7 @@ def test_struct_layouts_match_header():
     src = open(HEADER).read()
     for cname, cls in (("dfk_drop", _lib.Drop), ("dfk_view", _lib.View), ("dfk_gemm_args", _lib.GemmArgs),
                        ("dfk_wattn_args", _lib.WattnArgs), ("dfk_patch_embed_args", _lib.PatchEmbedArgs),
+                       ("dfk_conv2d_geo", _lib.Conv2dGeo),
                        ("dfk_wattn_bwd_args", _lib.WattnBwdArgs), ("dfk_im2col_args", _lib.Im2colArgs)):
         body = re.search(r"typedef struct \{([^{}]*)\}\s*" + cname + ";", src, flags=re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)

@@ -1,0 +1,126 @@
+"""GPU parity of the Inception-ResNet-v2 + NeXtVLAD video branch (IResNet.py:331-393,
+InceptionResV2.py) against the reference's own outputs (tests/golden/inception_b2t2.npz, B=2 clips x 2 frames x
+75x75, training-mode BatchNorm, dropout off): probabilities, BCE loss, every parameter gradient (strided sample +
+norm), BatchNorm running statistics after the step and the eval-mode probabilities that follow.
+fp32 parity mode within 2e-3 on probabilities / loss / running stats; gradients (through ~40 stacked train-mode
+BatchNorms, which amplify round-off) within 5e-2 for every parameter and 1e-2 for 95 % of them; bf16 within 5e-2
+on probabilities.
+Op-level checks: im2col/col2im, BatchNorm2d and pooling kernels against torch fp32."""
+import types
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import golden_cases as GC
+from fixtures import check, keys, load
+from oracle.fill import named_fill_, randn
+
+pytestmark = pytest.mark.gpu
+if torch.cuda.is_available():
+    from deepfake_amd import functional as Fn
+    from deepfake_amd.models import set_compute_dtype
+    from deepfake_amd.models.IResNet import InceptionVideoClassifier
+
+DEV = "cuda"
+
+
+def _model(dt):
+    c = GC.INCEPTION
+    args = types.SimpleNamespace(bn_momentum=0.1, num_frames=c["T"], classify_drop=0.0)
+    m = InceptionVideoClassifier(args, num_classes=1, drop_rate=0.0)
+    named_fill_(m, seed=c["seed"])
+    m = set_compute_dtype(m, dt).to(DEV)
+    x = randn(c["seed"] + 1, (c["B"], c["T"], 3, c["HW"], c["HW"])).to(DEV)
+    return c, m, x
+
+
+@pytest.mark.parametrize("dt,tol,gtol", [(torch.float32, 2e-3, 5e-2), (torch.bfloat16, 5e-2, None)])
+def test_inception_train_step_and_eval(dt, tol, gtol):
+    c, m, x = _model(dt)
+    fx = load(c["name"])
+    m.train()
+    prob = m(x)
+    loss = torch.nn.BCELoss()(prob.float(), torch.tensor([1.0, 0.0], device=DEV))
+    loss.backward()
+    check(fx, "prob", prob, tol)
+    assert abs(loss.item() - float(fx["loss"])) <= 2 * tol * abs(float(fx["loss"]))   # BCE of two probabilities
+    names = dict(m.named_parameters())
+    if gtol is not None:
+        gk = keys(fx, "g:")
+        assert len(gk) == sum(1 for p in m.parameters() if p.requires_grad)
+        from fixtures import error
+        # analytically zero gradients (their reference values are round-off): a bias feeding a softmax over a
+        # shift-invariant axis (NeXtVLAD bn0, IResNet.py:277-285) or a BatchNorm'd 1x1 conv
+        # (InceptionResV2.py:184: the last block's conv bias) -> checked in absolute terms
+        zero = {"g:video_nextvlad.bn0.bias", "g:inceptionRes.features.42.conv.bias"}
+        scale = max(float(names[k[2:]].grad.abs().max()) for k in gk)
+        for k in zero:
+            assert float(names[k[2:]].grad.abs().max()) < 1e-4 * scale, k
+        errs = sorted(((error(fx, k, names[k[2:]].grad), k) for k in gk if k not in zero), reverse=True)
+        assert errs[0][0] <= gtol, f"worst gradients: {errs[:5]}"
+        assert sum(e <= 1e-2 for e, _ in errs) >= 0.95 * len(errs), f"worst gradients: {errs[:20]}"
+    sd = m.state_dict()
+    for k in c["bn_keys"]:
+        check(fx, "s:" + k, sd[k], tol if dt == torch.float32 else 5e-2)
+    m.eval()
+    with torch.no_grad():
+        check(fx, "prob_eval", m(x), tol)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("k,s,p", [((3, 3), (2, 2), (0, 0)), ((1, 7), (1, 1), (0, 3)), ((5, 5), (1, 1), (2, 2)),
+                                   ((3, 3), (1, 1), (1, 1))])
+def test_conv_bn_relu_op(dt, k, s, p):
+    """Conv2d(bias=False) -> BatchNorm2d(train) -> ReLU on channels-last input vs torch fp32 (NCHW)."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    N, H, W, Cin, Cout = 4, 17, 15, 40, 48
+    x = torch.randn(N, H, W, Cin, device=DEV, generator=g)
+    x = x.to(dt).float()                      # the reference sees the same (bf16-rounded) input and weights
+    conv = torch.nn.Conv2d(Cin, Cout, k, stride=s, padding=p, bias=False).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(conv.weight.to(dt).float())
+    bn = torch.nn.BatchNorm2d(Cout, eps=1e-3, momentum=0.1).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    bn2 = torch.nn.BatchNorm2d(Cout, eps=1e-3, momentum=0.1).to(DEV)
+    bn2.load_state_dict(bn.state_dict())
+    w = conv.weight.detach().clone().requires_grad_(True)
+    gm = bn2.weight.detach().clone().requires_grad_(True)
+    bt = bn2.bias.detach().clone().requires_grad_(True)
+    xi = x.detach().clone().to(dt).requires_grad_(True)
+    y = Fn.ConvBNReLUFn.apply(xi, w, gm, bt, bn2, k, s, p, True)
+    xr = x.detach().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    ref = F.relu(bn(conv(xr))).permute(0, 2, 3, 1)
+    tol = 2e-5 if dt == torch.float32 else 3e-2
+    rel = lambda a, b: ((a.float() - b.float()).abs().max() / b.float().abs().max()).item()  # noqa: E731
+    assert rel(y, ref) < tol
+    rt = 1e-4 if dt == torch.float32 else 2e-2
+    assert rel(bn2.running_mean, bn.running_mean) < rt and rel(bn2.running_var, bn.running_var) < rt
+    dy = torch.randn(ref.shape, device=DEV, generator=g)
+    y.backward(dy.to(dt))
+    ref.backward(dy)
+    # bf16: the BatchNorm backward's mean subtraction cancels, so bf16 gradients are checked in norm (3e-2)
+    err = rel if dt == torch.float32 else (lambda a, b: ((a.float() - b.float()).norm() / b.float().norm()).item())
+    gt = 1e-4 if dt == torch.float32 else 3e-2
+    assert err(xi.grad.permute(0, 3, 1, 2), xr.grad) < gt
+    assert err(w.grad, conv.weight.grad) < gt
+    assert err(gm.grad, bn.weight.grad) < gt and err(bt.grad, bn.bias.grad) < gt
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_pool_op(mode):
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(3, 17, 16, 24, device=DEV, generator=g)
+    k, s, p = (3, 2, 0) if mode == 0 else (3, 1, 1)
+    xi = x.clone().requires_grad_(True)
+    y = Fn.Pool2dFn.apply(xi, k, s, p, mode)
+    xr = x.permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    ref = (F.max_pool2d(xr, k, s, p) if mode == 0 else
+           F.avg_pool2d(xr, k, s, p, count_include_pad=False)).permute(0, 2, 3, 1)
+    assert (y - ref).abs().max().item() < 1e-6
+    dy = torch.randn(ref.shape, device=DEV, generator=g)
+    y.backward(dy)
+    ref.backward(dy)
+    assert (xi.grad.permute(0, 3, 1, 2) - xr.grad).abs().max().item() < 1e-5

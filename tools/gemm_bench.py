@@ -48,6 +48,8 @@ def main():
         dw = torch.zeros(N, Kd, device="cuda")
         fl = 2.0 * M * N * Kd
         tf = t(lambda: K.linear(x, w, out=out))
+        aux = torch.empty(M, N, device="cuda", dtype=dt)
+        tg = t(lambda: K.linear(x, w, out=out, act=1, aux=aux))
         tx = t(lambda: K.linear_dx(dy, w, out=dx))
         tw = t(lambda: K.linear_dw(dy, x, dw))
         tot["fwd"] += tf
@@ -55,7 +57,8 @@ def main():
         tot["dw"] += tw
         bytes_f = (M * Kd + M * N + N * Kd) * x.element_size()
         print(f"{name:10s} M={M:7d} N={N:5d} K={Kd:5d}  fwd {fl / tf / 1e12:7.1f} TF ({bytes_f / tf / 1e9:6.0f} GB/s)"
-              f"  dx {fl / tx / 1e12:7.1f} TF  dw {fl / tw / 1e12:7.1f} TF   [{tf * 1e6:.0f}/{tx * 1e6:.0f}/{tw * 1e6:.0f} us]",
+              f"  dx {fl / tx / 1e12:7.1f} TF  dw {fl / tw / 1e12:7.1f} TF   [{tf * 1e6:.0f}/{tx * 1e6:.0f}/{tw * 1e6:.0f} us]"
+              f"  gelu+aux {tg * 1e6:.0f} us",
               flush=True)
         if a.torch:
             rf = t(lambda: torch.nn.functional.linear(x, w))
