@@ -27,16 +27,19 @@ constexpr int WRES_LIMIT = 49152;      // W slice elements (96 KiB bf16) -> one 
 constexpr int NT = 512;                // 8 waves x 16 token rows = 128-row tiles
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <int KC, int NBW, int NSPLIT>
 constexpr int wres_lds() { return (NBW * 16 * NSPLIT * (KC * 32 + 8) + 8 * 16 * (NBW * 16 + 8)) * 2; }
 
-// two workgroups per CU (4 waves per SIMD, <= 128 VGPRs) only for the smallest wave tile: every other
-// variant spills at 128 VGPRs
+// one 8-wave workgroup per CU (2 waves per SIMD, <= 256 VGPRs)
 template <int KC, int NBW, int NSPLIT>
-constexpr bool wres_two_per_cu() { return KC == 3 && NBW == 6 && NSPLIT == 1 && wres_lds<KC, NBW, NSPLIT>() <= 80 * 1024; }
+constexpr bool wres_two_per_cu() { return false; }   // the 128-VGPR variant spilled (the epilogue's loads in flight)
 
-template <int KC, int NBW, int NSPLIT>
+// ACT: 0 plain, 1 GELU (pre-activation -> aux), 2 times gelu'(aux) — a template so the epilogue has no
+// data-dependent branches around its loads (a branch around a load makes the compiler wait vmcnt(0) there,
+// and vmcnt also counts the previous tile's stores)
+template <int KC, int NBW, int NSPLIT, int ACT>
 __global__ __launch_bounds__(512, (wres_two_per_cu<KC, NBW, NSPLIT>() ? 4 : 2))
 void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   // slice of BN = NSPLIT*NBW*16 output channels; the 8 waves form (8/NSPLIT) row groups x NSPLIT column
@@ -47,8 +50,6 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   __shared__ __attribute__((aligned(16))) bf16raw w_lds[BN * WS + 8 * 16 * SS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   bf16raw* stg = w_lds + BN * WS + wave * 16 * SS;
-  const bool staged = g.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0 && g.N % 8 == 0 &&
-                      (!g.aux || (g.ldaux % 8 == 0 && (reinterpret_cast<uintptr_t>(g.aux) & 15) == 0));
   const int rg = wave / NSPLIT, cg = wave % NSPLIT;
   const int slice = blockIdx.x % nslices;
   const int n0 = slice * BN;
@@ -83,6 +84,21 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   const int mrow = lane & 15, kq = (lane >> 4) * 8, nq = (lane >> 4) * 4;
   const DropCtx dc = drop_ctx(g.drop);   // dropout / DropPath of the output (mode 0: none)
   const bf16raw* wbase = w_lds + (cg * NBW * 16 + mrow) * WS + kq;
+  const int c0 = n0 + cg * NBW * 16;                    // first channel of this wave's columns
+  // absent bias / residual: read C itself (always valid memory) and clear the bits (C may hold NaN patterns,
+  // so no multiply-by-zero), so every epilogue load is unconditional (channels clamped into range)
+  const bf16raw* bsrc = bias ? bias : C;
+  const uint32_t bmask = bias ? 0xffffffffu : 0u;
+  const bf16raw* rsrc = res ? res : C;
+  const long rld = res ? g.ldr : g.ldc;
+  const uint32_t rmask = res ? 0xffffffffu : 0u;
+  // buffer descriptors of the outputs: exactly the M rows (bounds-checked stores)
+  auto rsrc_of = [&](void* p, long ld) {
+    const long bytes = (long)g.M * ld * 2;
+    return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rC = rsrc_of(C, g.ldc);
+  const __amdgpu_buffer_rsrc_t rAux = rsrc_of(aux ? (void*)aux : (void*)C, aux ? g.ldaux : g.ldc);
 
   // this wave's fragment row of tile t: token m = t*ROWS_T + rg*16 + (lane&15)
   auto load_a = [&](int t, uint4 (&fr)[KC]) {
@@ -97,9 +113,24 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
     }
   };
 
-  auto process = [&](int t, const uint4 (&a_cur)[KC]) {
+  constexpr int NAX = ACT == 2 ? NBW : 1;
+  // the tile's epilogue operands (bias, residual, gelu input): requested BEFORE the next tile's A prefetch,
+  // so the epilogue's waits on them (vmcnt counts in issue order) leave that prefetch in flight
+  auto load_epi = [&](int t, uint2 (&bb)[NBW], uint2 (&rr)[NBW], uint2 (&ax)[NAX]) {
     const long m = (long)t * ROWS_T + rg * 16 + mrow;
-    const bool mok = m < g.M;
+    const long mc = m < g.M ? m : g.M - 1;               // clamped row (the store mask drops the tail)
+#pragma unroll
+    for (int nb = 0; nb < NBW; ++nb) {
+      const int n = min(c0 + nb * 16 + nq, g.N - 4);
+      bb[nb] = *reinterpret_cast<const uint2*>(bsrc + n);
+      rr[nb] = *reinterpret_cast<const uint2*>(rsrc + mc * rld + n);
+      if constexpr (ACT == 2) ax[nb] = *reinterpret_cast<const uint2*>(aux + mc * g.ldaux + n);
+    }
+  };
+
+  auto process = [&](int t, const uint4 (&a_cur)[KC], const uint2 (&bb)[NBW], const uint2 (&rr)[NBW],
+                     const uint2 (&ax)[NAX]) {
+    const long m = (long)t * ROWS_T + rg * 16 + mrow;
 
     f32x4 acc[NBW];
 #pragma unroll
@@ -125,61 +156,62 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
     // ---- epilogue: lane holds channels n0 + (cg*NBW + nb)*16 + nq .. +3 of token m.  Outputs go through
     // a per-wave LDS tile so that global stores are whole 16-B chunks of token rows (8-B stores scattered
     // over 16 rows per instruction ran the write-heavy launches at 2.2-2.8 TB/s)
+    auto bias4 = [&](int nb, float (&v)[4]) {
+      const uint2 b = make_uint2(bb[nb].x & bmask, bb[nb].y & bmask);
+      v[0] = acc[nb][0] + __uint_as_float(b.x << 16); v[1] = acc[nb][1] + __uint_as_float(b.x & 0xffff0000u);
+      v[2] = acc[nb][2] + __uint_as_float(b.y << 16); v[3] = acc[nb][3] + __uint_as_float(b.y & 0xffff0000u);
+    };
     const long mt0 = (long)t * ROWS_T + rg * 16;          // first token of this wave's tile
-    const int c0 = n0 + cg * NBW * 16;                    // first channel of this wave's columns
-    auto flush = [&](bf16raw* dst, long ld) {              // staged [16][NBW*16] tile -> dst rows
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // LDS-only wave syncs: a release fence would also wait vmcnt(0), i.e. for the next tile's A prefetch
+    auto lds_sync = [] {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // staged [16][NBW*16] tile -> dst rows by buffer stores: rows past M fall outside the descriptor's range
+    // and columns past N get an out-of-range offset, so the hardware drops them and no branch surrounds a
+    // store (a branch around a store makes hipcc wait vmcnt(0) — for the A prefetch too — after it)
+    auto flush = [&](__amdgpu_buffer_rsrc_t rs, long ld) {
+      lds_sync();
       constexpr int CPR = NBW * 2;                          // 16-B chunks per row
 #pragma unroll
       for (int c = lane; c < 16 * CPR; c += 64) {
         const int r = c / CPR, ch = (c % CPR) * 8;
-        const uint4 u = *reinterpret_cast<const uint4*>(stg + r * SS + ch);
-        if (mt0 + r < g.M && c0 + ch < g.N) *reinterpret_cast<uint4*>(dst + (mt0 + r) * ld + c0 + ch) = u;
+        const u32x4 u = *reinterpret_cast<const u32x4*>(stg + r * SS + ch);
+        const long e = (mt0 + r) * ld + c0 + ch;            // element offset
+        const uint32_t off = (c0 + ch < g.N && e < 0x7fffffffL) ? (uint32_t)(e * 2) : 0xfffffff0u;
+        __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 0);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // reads done before the tile is rewritten
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      lds_sync();                                         // reads done before the tile is rewritten
     };
     auto put = [&](int nb, const float (&v)[4], bf16raw* dst, long ld) {
       uint2 o;
       o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
       o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      if (staged) *reinterpret_cast<uint2*>(stg + mrow * SS + nb * 16 + nq) = o;
-      else if (mok && c0 + nb * 16 + nq < g.N) *reinterpret_cast<uint2*>(dst + m * ld + c0 + nb * 16 + nq) = o;
+      *reinterpret_cast<uint2*>(stg + mrow * SS + nb * 16 + nq) = o;   // (dfk_wres_try guarantees staging)
     };
-    if (g.act == 1 && aux) {        // the pre-activation (GELU backward input) first
+    if constexpr (ACT == 1) {       // the pre-activation (GELU backward input) first
+      if (aux) {
 #pragma unroll
-      for (int nb = 0; nb < NBW; ++nb) {
-        const int n = c0 + nb * 16 + nq;
-        float v[4] = {acc[nb][0], acc[nb][1], acc[nb][2], acc[nb][3]};
-        if (bias && n < g.N) {
-          const uint2 b = *reinterpret_cast<const uint2*>(bias + n);
-          v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
-          v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
+        for (int nb = 0; nb < NBW; ++nb) {
+          float v[4];
+          bias4(nb, v);
+          put(nb, v, aux, g.ldaux);
         }
-        put(nb, v, aux, g.ldaux);
+        flush(rAux, g.ldaux);
       }
-      if (staged) flush(aux, g.ldaux);
     }
     {
       const float gmul = dc.mode == 2 ? drop_mul(dc, m, 0) : 1.f;   // DropPath: one draw per token group
 #pragma unroll
       for (int nb = 0; nb < NBW; ++nb) {
         const int n = c0 + nb * 16 + nq;
-        const bool ok = mok && n < g.N;
-        float v[4] = {acc[nb][0], acc[nb][1], acc[nb][2], acc[nb][3]};
-        if (bias && n < g.N) {
-          const uint2 b = *reinterpret_cast<const uint2*>(bias + n);
-          v[0] += __uint_as_float(b.x << 16); v[1] += __uint_as_float(b.x & 0xffff0000u);
-          v[2] += __uint_as_float(b.y << 16); v[3] += __uint_as_float(b.y & 0xffff0000u);
-        }
-        if (g.act == 1) {
+        float v[4];
+        bias4(nb, v);
+        if constexpr (ACT == 1) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
-        } else if (g.act == 2 && ok) {
-          const uint2 a = *reinterpret_cast<const uint2*>(aux + m * g.ldaux + n);
+        } else if constexpr (ACT == 2) {
+          const uint2 a = ax[nb];
           v[0] *= dgelu_f(__uint_as_float(a.x << 16)); v[1] *= dgelu_f(__uint_as_float(a.x & 0xffff0000u));
           v[2] *= dgelu_f(__uint_as_float(a.y << 16)); v[3] *= dgelu_f(__uint_as_float(a.y & 0xffff0000u));
         }
@@ -190,40 +222,54 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] *= drop_mul(dc, m, n + e);
         }
-        if (res && ok) {
-          const uint2 r = *reinterpret_cast<const uint2*>(res + m * g.ldr + n);
-          v[0] += __uint_as_float(r.x << 16); v[1] += __uint_as_float(r.x & 0xffff0000u);
-          v[2] += __uint_as_float(r.y << 16); v[3] += __uint_as_float(r.y & 0xffff0000u);
-        }
+        const uint2 r = make_uint2(rr[nb].x & rmask, rr[nb].y & rmask);
+        v[0] += __uint_as_float(r.x << 16); v[1] += __uint_as_float(r.x & 0xffff0000u);
+        v[2] += __uint_as_float(r.y << 16); v[3] += __uint_as_float(r.y & 0xffff0000u);
         put(nb, v, C, g.ldc);
-        if (nb % 4 == 3) __builtin_amdgcn_sched_barrier(0);   // bound the epilogue loads hoisted ahead
       }
-      if (staged) flush(C, g.ldc);
+      flush(rC, g.ldc);
     }
   };
 
-  // the next tile's A fragments are in flight while this tile computes (deeper register queues of A
-  // tiles spilled: the unrolled process() bodies get interleaved by the scheduler)
+  // A fragments of the next DEPTH tiles are in flight while a tile computes (a register ring: 2 deep for the
+  // K = 96 Linears of Swin stage 1, whose tiles are shortest; deeper rings spilled).  The loop body handles
+  // DEPTH tiles with no exit in between: a tile index past the end computes on clamped loads and its stores
+  // fall outside the output descriptor (rows >= M), so no branch surrounds a load or a store.
+  constexpr int DEPTH = (KC == 3 && NBW == 6) ? 2 : 1;
   int t = blockIdx.x / nslices;
-  uint4 a_nxt[KC];
-  if (t < ntiles) load_a(t, a_nxt);
-  for (; t < ntiles; t += stride) {
+  uint4 a0[KC], a1[KC];
+  load_a(min(t, ntiles - 1), a0);
+  if constexpr (DEPTH == 2) load_a(min(t + stride, ntiles - 1), a1);
+  auto step = [&](uint4 (&buf)[KC], int tt) {
     uint4 cur[KC];
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) cur[kc] = a_nxt[kc];
-    if (t + stride < ntiles) load_a(t + stride, a_nxt);
-    process(t, cur);
+    for (int kc = 0; kc < KC; ++kc) cur[kc] = buf[kc];
+    uint2 bb[NBW], rr[NBW], ax[NAX];
+    load_epi(tt, bb, rr, ax);
+    load_a(min(tt + DEPTH * stride, ntiles - 1), buf);
+    process(tt, cur, bb, rr, ax);
+  };
+  for (; t < ntiles; t += DEPTH * stride) {
+    step(a0, t);
+    if constexpr (DEPTH == 2) {
+      __builtin_amdgcn_sched_barrier(0);
+      step(a1, t + stride);
+    }
   }
 }
 
 template <int KC, int NBW, int NSPLIT>
 void launch_wres(const dfk_gemm_args& g, int nslices, hipStream_t s) {
+  static_assert(NT == 512, "8-wave workgroups");
   // persistent grid: as many 8-wave workgroups per CU as the W slice's LDS allows (1 or 2), a multiple
   // of the slice count so every workgroup keeps one slice for its whole life
   constexpr int per_cu = wres_two_per_cu<KC, NBW, NSPLIT>() ? 2 : 1;
   const int ntiles = dfk_cdiv(g.M, 16 * (8 / NSPLIT));
   const int per = std::max(1, std::min(ntiles, 256 * per_cu / nslices));
-  hipLaunchKernelGGL((wres_kernel<KC, NBW, NSPLIT>), dim3(per * nslices), dim3(NT), 0, s, g, nslices, ntiles);
+  const dim3 grid(per * nslices);
+  if (g.act == 1) hipLaunchKernelGGL((wres_kernel<KC, NBW, NSPLIT, 1>), grid, dim3(NT), 0, s, g, nslices, ntiles);
+  else if (g.act == 2) hipLaunchKernelGGL((wres_kernel<KC, NBW, NSPLIT, 2>), grid, dim3(NT), 0, s, g, nslices, ntiles);
+  else hipLaunchKernelGGL((wres_kernel<KC, NBW, NSPLIT, 0>), grid, dim3(NT), 0, s, g, nslices, ntiles);
 }
 
 bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
@@ -243,6 +289,8 @@ int dfk_wres_try(const dfk_gemm_args& g, hipStream_t s) {
       (g.aux && (g.ldaux % 4 || !al8(g.aux))))
     return 0;
   if (g.b_kmajor && g.N % 8) return 0;
+  // outputs leave through the per-wave LDS staging tile as whole 16-B chunks of token rows
+  if (g.ldc % 8 || ((uintptr_t)g.c & 15) || g.N % 8 || (g.aux && (g.ldaux % 8 || ((uintptr_t)g.aux & 15)))) return 0;
   const int KC = g.K / 32;
   // widest slice (fewest A re-reads) that fits WRES_LIMIT, then the least padding among equal counts
   int best = 0, best_sl = 1 << 30, best_waste = 1 << 30;
