@@ -28,7 +28,10 @@ constexpr int NT = 256, MAXT = 64;     // 4 waves x 16 tokens: token rows of up 
 
 struct PeGeo {
   int Do, Ho, Wo, Ws;                  // Ws: slab row stride (floats)
+  int xbytes;                          // bytes of the clip batch (buffer-descriptor range)
 };
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // register-staged slab: each thread's share of the token row's 24 input rows (float4 chunks), so the next
 // row's loads are in flight while the current row computes (persistent forward)
@@ -41,27 +44,22 @@ __device__ __forceinline__ void slab_load(const dfk_patch_embed_args& a, const P
   const int d = (int)(r2 % g.Do);
   const long b = r2 / g.Do;
   const int q4 = g.Wo;
-  const float* x = reinterpret_cast<const float*>(a.x);
+  // branch-free (W % 4 == 0, pe_geo): buffer loads through a descriptor of the whole clip batch; a chunk
+  // past T / H (F.pad) or past the row's 24 x Wo chunks gets an out-of-range offset and reads as zero, so
+  // all SLAB_REGS loads are in flight together (a branch around a load makes hipcc wait for it there)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), (short)0, g.xbytes,
+                                                                      0x00020000);
 #pragma unroll
   for (int j = 0; j < SLAB_REGS; ++j) {
     const int i = threadIdx.x + j * NT;
-    v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < SROWS * q4) {
-      const int sr = i / q4, x0 = (i - sr * q4) * 4;
-      const int c = sr / 8, kd = (sr / 4) % 2, kh = sr % 4;
-      const int t = d * 2 + kd, y = h * 4 + kh;
-      if (t < a.T && y < a.H) {
-        const float* p = x + b * a.sb + c * a.sc + (long)t * a.st + (long)y * a.sh + x0;
-        if (x0 + 4 <= a.W) {
-          v[j] = *reinterpret_cast<const float4*>(p);
-        } else {
-          float e[4] = {0.f, 0.f, 0.f, 0.f};
-          for (int k = 0; k < 4; ++k)
-            if (x0 + k < a.W) e[k] = p[k];
-          v[j] = make_float4(e[0], e[1], e[2], e[3]);
-        }
-      }
-    }
+    const int sr = i / q4, x0 = (i - sr * q4) * 4;
+    const int c = sr / 8, kd = (sr / 4) % 2, kh = sr % 4;
+    const int t = d * 2 + kd, y = h * 4 + kh;
+    const bool ok = i < SROWS * q4 && t < a.T && y < a.H;
+    const long e = b * a.sb + c * a.sc + (long)t * a.st + (long)y * a.sh + x0;
+    const uint32_t off = ok ? (uint32_t)(e * 4) : 0xfffffff0u;
+    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    v[j] = make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3]));
   }
 }
 
@@ -148,9 +146,34 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
+// bias / LN gamma / LN beta of this lane's channels nb*16 + 4*(lane>>4) + r, loaded once per workgroup
+// (per-row global loads would make every row wait for the next row's clip prefetch: vmcnt is in order)
+template <int NB>
+struct PeParams {
+  float b[NB][4], g[NB][4], t[NB][4];
+};
+
+template <int NB>
+__device__ __forceinline__ PeParams<NB> load_params(const dfk_patch_embed_args& a) {
+  PeParams<NB> P;
+  const int nq = ((threadIdx.x & 63) >> 4) * 4;
+  const bf16raw* bias = reinterpret_cast<const bf16raw*>(a.b);
+  const bf16raw* gam = reinterpret_cast<const bf16raw*>(a.ln_w);
+  const bf16raw* bet = reinterpret_cast<const bf16raw*>(a.ln_b);
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      P.b[nb][r] = bf2f(bias[nb * 16 + nq + r]);
+      P.g[nb][r] = bf2f(gam[nb * 16 + nq + r]);
+      P.t[nb][r] = bf2f(bet[nb * 16 + nq + r]);
+    }
+  return P;
+}
+
 template <int NB>
 __device__ __forceinline__ void pe_fwd_row(const dfk_patch_embed_args& a, const PeGeo& g, long row, const float* slab,
-                                           const bf16raw* w_lds, bf16raw* stg_all) {
+                                           const bf16raw* w_lds, bf16raw* stg_all, const PeParams<NB>& P) {
   constexpr int C = NB * 16, SS = C + 8;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mrow = lane & 15, nq = (lane >> 4) * 4;
@@ -158,15 +181,12 @@ __device__ __forceinline__ void pe_fwd_row(const dfk_patch_embed_args& a, const 
   if (wave * 16 >= g.Wo) return;                   // idle wave: no barrier inside this function
   f32x4 acc[NB];
   conv_tokens<NB>(slab, g.Ws, w_lds, w < g.Wo ? w : 0, acc);
-  const bf16raw* bias = reinterpret_cast<const bf16raw*>(a.b);
-  const bf16raw* gam = reinterpret_cast<const bf16raw*>(a.ln_w);
-  const bf16raw* bet = reinterpret_cast<const bf16raw*>(a.ln_b);
   float s = 0.f;
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      acc[nb][r] += bf2f(bias[nb * 16 + nq + r]);
+      acc[nb][r] += P.b[nb][r];
       s += acc[nb][r];
     }
   const float mean = group_sum(s) * (1.f / C);
@@ -186,7 +206,7 @@ __device__ __forceinline__ void pe_fwd_row(const dfk_patch_embed_args& a, const 
     const int n = nb * 16 + nq;
     float v[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = (acc[nb][r] - mean) * rstd * bf2f(gam[n + r]) + bf2f(bet[n + r]);
+    for (int r = 0; r < 4; ++r) v[r] = (acc[nb][r] - mean) * rstd * P.g[nb][r] + P.t[nb][r];
     uint2 o;
     o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
     o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
@@ -208,7 +228,7 @@ __device__ __forceinline__ void pe_fwd_row(const dfk_patch_embed_args& a, const 
   }
 }
 
-template <int NB>
+template <int NB, int DEPTH>
 __global__ __launch_bounds__(NT) void pe_fwd_kernel(const dfk_patch_embed_args a, const PeGeo g, long nrows) {
   constexpr int C = NB * 16, SS = C + 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -216,16 +236,26 @@ __global__ __launch_bounds__(NT) void pe_fwd_kernel(const dfk_patch_embed_args a
   bf16raw* stg_all = w_lds + C * PKS;
   float* slab = reinterpret_cast<float*>(stg_all + 4 * 16 * SS);
   load_weight<NB>(a, w_lds);
-  // persistent over token rows: row r+grid's clip rows are loaded into registers while row r computes
-  float4 nxt[SLAB_REGS];
+  const PeParams<NB> P = load_params<NB>(a);
+  // persistent over token rows: the clip rows of the next DEPTH token rows (r + G, r + 2G) stream into
+  // registers while row r computes
+  const long G = gridDim.x;
+  float4 b0[SLAB_REGS], b1[SLAB_REGS];
   long r = blockIdx.x;
-  if (r < nrows) slab_load(a, g, r, nxt);
-  for (; r < nrows; r += gridDim.x) {
+  if (r < nrows) slab_load(a, g, r, b0);
+  if (DEPTH == 2 && r + G < nrows) slab_load(a, g, r + G, b1);
+  auto step = [&](float4 (&cur)[SLAB_REGS]) {
     __syncthreads();                               // the previous row's slab reads are done
-    slab_store(g, nxt, slab);
+    slab_store(g, cur, slab);
     __syncthreads();
-    if (r + gridDim.x < nrows) slab_load(a, g, r + gridDim.x, nxt);
-    pe_fwd_row<NB>(a, g, r, slab, w_lds, stg_all);
+    if (r + DEPTH * G < nrows) slab_load(a, g, r + DEPTH * G, cur);
+    pe_fwd_row<NB>(a, g, r, slab, w_lds, stg_all, P);
+    r += G;
+  };
+  while (r < nrows) {
+    step(b0);
+    if (DEPTH == 1 || r >= nrows) continue;
+    step(b1);
   }
 }
 
@@ -348,7 +378,11 @@ bool pe_geo(const dfk_patch_embed_args& a, PeGeo& g) {
   g.Ho = (a.H + 3) / 4;
   g.Wo = (a.W + 3) / 4;
   g.Ws = g.Wo * 4 + 4;
-  return g.Wo <= MAXT;
+  // extent of the clip batch (the largest element offset + 1), for the loads' bounds check
+  const long last = (long)(a.B - 1) * a.sb + 2L * a.sc + (long)(a.T - 1) * a.st + (long)(a.H - 1) * a.sh + a.W;
+  if (last * 4 >= 0x7fffffffL) return false;
+  g.xbytes = (int)(last * 4);
+  return g.Wo <= MAXT && a.W % 4 == 0;
 }
 
 size_t pe_lds_fwd(int C, const PeGeo& g) { return (size_t)C * PKS * 2 + 4 * 16 * (C + 8) * 2 + (size_t)SROWS * g.Ws * 4; }
@@ -366,11 +400,17 @@ extern "C" int dfk_patch_embed_fwd(const dfk_patch_embed_args* ap, hipStream_t s
   const long rows = (long)a.B * g.Do * g.Ho;
   const size_t lds = pe_lds_fwd(a.C, g);
   if (lds > 64 * 1024) return DFK_EINVAL;
-  const unsigned grid = (unsigned)std::min<long>(rows, 512);   // persistent: two workgroups per CU
-  if (a.C == 96)
-    hipLaunchKernelGGL(pe_fwd_kernel<6>, dim3(grid), dim3(NT), lds, s, a, g, rows);
-  else
-    hipLaunchKernelGGL(pe_fwd_kernel<8>, dim3(grid), dim3(NT), lds, s, a, g, rows);
+  // persistent: two workgroups per CU (tuning knobs DFK_PE_PERCU / DFK_PE_DEPTH for tools/pe_bench.py)
+  static const int env_cu = getenv("DFK_PE_PERCU") ? atoi(getenv("DFK_PE_PERCU")) : 2;
+  static const int depth = getenv("DFK_PE_DEPTH") ? atoi(getenv("DFK_PE_DEPTH")) : 2;
+  const unsigned grid = (unsigned)std::min<long>(rows, 256L * std::max(1, env_cu));
+  if (a.C == 96) {
+    if (depth == 1) hipLaunchKernelGGL((pe_fwd_kernel<6, 1>), dim3(grid), dim3(NT), lds, s, a, g, rows);
+    else hipLaunchKernelGGL((pe_fwd_kernel<6, 2>), dim3(grid), dim3(NT), lds, s, a, g, rows);
+  } else {
+    if (depth == 1) hipLaunchKernelGGL((pe_fwd_kernel<8, 1>), dim3(grid), dim3(NT), lds, s, a, g, rows);
+    else hipLaunchKernelGGL((pe_fwd_kernel<8, 2>), dim3(grid), dim3(NT), lds, s, a, g, rows);
+  }
   DFK_CHECK_LAUNCH();
   return 0;
 }

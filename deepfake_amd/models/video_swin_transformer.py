@@ -231,6 +231,7 @@ class PatchEmbed3D(nn.Module):
         return (self.compute_dtype == torch.bfloat16 and self.norm is not None and self.in_chans == 3 and
                 self.patch_size == (2, 4, 4) and self.embed_dim in (96, 128) and x.dtype == torch.float32 and
                 x.stride(-1) == 1 and all(s % 4 == 0 for s in x.stride()[:-1]) and x.shape[-1] <= 256 and
+                x.shape[-1] % 4 == 0 and
                 x.data_ptr() % 16 == 0 and not getattr(self, "force_unfused", False))
 
     def tokens(self, x, layout="bcthw"):
