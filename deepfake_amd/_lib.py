@@ -10,7 +10,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdfk.so")
+LIB_PATH = os.environ.get("DFK_LIB") or os.path.join(_HERE, "libdfk.so")   # DFK_LIB: experiment builds (tools/exp_build.sh)
 
 F32, BF16 = 0, 1
 

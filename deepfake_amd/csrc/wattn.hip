@@ -122,11 +122,13 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr int kBwdWaves = 8;
 constexpr int kSdStride = 40;  // bf16 row stride of the per-wave dS^T scratch [32 keys][32 queries]
 
-// element offset of (row, col) in a [rows][HD] bf16 tile with 16-B chunks XOR-swizzled by row:
-// conflict-free 16-B row reads (A operands) and 8-B transposed reads (tr16 B operands)
+// element offset of (row, col) in a [rows][HD] bf16 tile with 16-B chunks XOR-swizzled by row.  HD 32:
+// chunk ^= (-(row >> 2)) & 3 makes the three access shapes conflict-free on the gfx950 lane groups (16-B
+// A-operand row reads: lanes 16 rows x 4 chunks; 8-B tr16 reads: 8 rows x 4 column pairs; 16-B staging
+// writes) — checked by brute force over the lane groups; HD 64: 2-way on the row and tr16 reads.
 template <int HD>
 __device__ __forceinline__ int swz(int row, int col) {
-  const int f = HD == 32 ? ((row & 2) | ((row >> 2) & 1)) : (((row & 3) << 1) | ((row >> 2) & 1));
+  const int f = HD == 32 ? ((4 - ((row >> 2) & 3)) & 3) : (((row & 3) << 1) | ((row >> 2) & 1));
   return row * HD + (((col >> 3) ^ f) << 3) + (col & 7);
 }
 
@@ -743,7 +745,11 @@ __global__ __launch_bounds__(256) void wattn_fwd_tab_kernel(const dfk_wattn_args
     const f32x4* tq0 = reinterpret_cast<const f32x4*>(tch) + ((long)(qb * 2) * nkb * 64 + lane) * 2;
     const long tqh = (long)nkb * 64 * 2;   // f32x4 stride between the two query halves
     auto load_tab = [&](f32x4 (&s)[2][2], int kb) {
+#ifdef DFK_EXP_TABFIX
+      const f32x4* p = reinterpret_cast<const f32x4*>(tch) + lane * 2 + 0 * kb;
+#else
       const f32x4* p = tq0 + (long)kb * 128;
+#endif
 #pragma unroll
       for (int qh = 0; qh < 2; ++qh) {
         s[qh][0] = p[qh * tqh];
@@ -783,7 +789,11 @@ __global__ __launch_bounds__(256) void wattn_fwd_tab_kernel(const dfk_wattn_args
         const float x0 = max3f(s[qh][0][0], s[qh][0][1], s[qh][0][2]);
         const float x1 = max3f(s[qh][0][3], s[qh][1][0], s[qh][1][1]);
         const float x2 = max3f(s[qh][1][2], s[qh][1][3], x0);
+#ifdef DFK_EXP_NOMAX
+        const float mx = 0.f * (x1 + x2);
+#else
         const float mx = grp_max4(fmaxf(x1, x2)) * scale2;
+#endif
         mnew[qh] = mx > m2[qh] + kRescale ? mx : m2[qh];
         grow |= mnew[qh] != m2[qh];
       }
@@ -804,7 +814,11 @@ __global__ __launch_bounds__(256) void wattn_fwd_tab_kernel(const dfk_wattn_args
         for (int h2 = 0; h2 < 2; ++h2)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
+#ifdef DFK_EXP_NOEXP
+            pf[qh][h2 * 4 + r] = (__bf16)(__builtin_fmaf(s[qh][h2][r], scale2, -m2[qh]));
+#else
             pf[qh][h2 * 4 + r] = (__bf16)__builtin_amdgcn_exp2f(__builtin_fmaf(s[qh][h2][r], scale2, -m2[qh]));
+#endif
       load_tab(s, min(kb + 2, nkb - 1));   // unconditional (clamped): static vmcnt counts, no phi copies
       // DROP: O accumulates the dropped probabilities, the denominator l the undropped ones
       bf16x8 pv[2] = {pf[0], pf[1]};
@@ -1624,6 +1638,280 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
   }
 }
 
+// Backward with the bias tables, one launch over all Np queries of the window (Q, dO resident in LDS).
+// One workgroup = one (clip, window, head); wave w owns key blocks w, w + nwaves (dK, dV in registers) and
+// sweeps every query block, STAGGERED: at step i wave w takes query block (i + w) mod nqb, so at any step the
+// waves touch distinct query blocks of the fp32 dQ accumulator in LDS and add their partial dQ = dS K into it
+// with a plain read-add-write; one barrier per step keeps the waves in step, so the add order per element is
+// fixed (deterministic).  (LDS float atomics instead of the barrier measured 3x slower.)  The table tile of the next step is
+// loaded one step ahead; no global read-modify-write inside the sweep.  dS^T still goes to the global
+// scratch (dsg) for the dRPB reduction.
+template <int HD, bool DROP>
+__global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_tab_kernel(const dfk_wattn_bwd_args ba, const Geo g,
+                                                            bf16raw* __restrict__ dsg,
+                                                            const float* __restrict__ tabb) {
+  const dfk_wattn_args& a = ba.f;
+  const int nwaves = blockDim.x >> 6;
+  const int Np = g.Np, nkb = Np / 32, nqb = Np / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* p = smem;
+  float* dQa = reinterpret_cast<float*>(p); p += 4 * (size_t)Np * HD;   // per 32-query block: [qh][et][lane][4]
+  bf16raw* Qs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;
+  bf16raw* dOs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;
+  bf16raw* Sd = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)nwaves * 32 * kSdStride;
+  int* trow = reinterpret_cast<int*>(p); p += 4 * Np;
+  float* lse2 = reinterpret_cast<float*>(p); p += 4 * Np;   // lse * log2(e); +inf beyond N
+  float* delta = reinterpret_cast<float*>(p);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = lane >> 4, ql = lane & 15, tq = ql >> 2, tp = ql & 3;
+  int unit = blockIdx.x;
+  const int head = unit % a.heads;
+  unit /= a.heads;
+  const int win = unit % g.nW, b = unit / g.nW;
+  const int hoff = head * HD;
+  const f32x4* tch = reinterpret_cast<const f32x4*>(tabb) +
+                     ((long)win_class(a, g, win) * a.heads + head) * (long)Np * Np / 4 + lane * 4;
+
+  for (int i = tid; i < Np; i += blockDim.x) {
+    trow[i] = token_info_row(a, g, b, win, i);
+    lse2[i] = i < g.N ? a.lse[(long)blockIdx.x * Np + i] * kLog2e : INFINITY;
+  }
+  for (int i = tid * 4; i < Np * HD; i += blockDim.x * 4) *reinterpret_cast<f32x4*>(dQa + i) = f32x4{0, 0, 0, 0};
+  __syncthreads();
+  constexpr int CH = HD / 8;
+  for (int base = 0; base < Np * CH; base += blockDim.x) {
+    const int idx = base + tid;
+    float d = 0.f;
+    if (idx < Np * CH) {
+      const int li = idx / CH, c = (idx % CH) * 8;
+      const int row = trow[li];
+      const uint4 qv = tok_ld16<bf16raw>(a.q, a.pad_q, row, a.ld_qkv, hoff + c);
+      const uint4 dv = tok_ld16<bf16raw>(ba.dout, nullptr, row, ba.ld_dout, hoff + c);
+      const uint4 ov = tok_ld16<bf16raw>(a.out, nullptr, row, a.ld_out, hoff + c);
+      d = dot8_bf16(ov, dv);
+      *reinterpret_cast<uint4*>(Qs + swz<HD>(li, c)) = qv;
+      *reinterpret_cast<uint4*>(dOs + swz<HD>(li, c)) = dv;
+    }
+#pragma unroll
+    for (int o = 1; o < CH; o <<= 1) d += __shfl_xor(d, o, 64);
+    if (idx < Np * CH && (idx % CH) == 0) delta[idx / CH] = d;
+  }
+  __syncthreads();
+
+  bf16raw* Sw = Sd + wave * 32 * kSdStride;
+  const float scale2 = a.scale * kLog2e;
+  const DropCtx dc = drop_ctx(a.drop);
+  bf16raw* dsu = dsg ? dsg + (long)blockIdx.x * Np * Np : nullptr;   // this window-head's dS^T [k][q]
+  for (int pass = 0; pass * nwaves < nkb; ++pass) {
+    const int kb = pass * nwaves + wave;
+    if (kb >= nkb) {   // no key block this pass: keep the step barriers
+#ifndef DFK_EXP_NOBAR
+      for (int i = 0; i < nqb; ++i) __syncthreads();
+#endif
+      continue;
+    }
+    bf16x8 kB[2][HD / 32], vB[2][HD / 32], kN[HD / 16];
+    f32x4 dK[2][HD / 16], dV[2][HD / 16];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int row = trow[kb * 32 + h2 * 16 + ql];
+#pragma unroll
+      for (int es = 0; es < HD / 32; ++es) {
+        kB[h2][es] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + es * 32 + grp * 8));
+        vB[h2][es] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + es * 32 + grp * 8));
+      }
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et) { dK[h2][et] = f32x4{0, 0, 0, 0}; dV[h2][et] = f32x4{0, 0, 0, 0}; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = trow[kb * 32 + grp * 8 + j];
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et)
+        kN[et][j] = __builtin_bit_cast(__bf16, tok_ld1<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + ql + et * 16));
+    }
+    auto tab_tile = [&](f32x4 (&t)[2][2], int qb) {
+#ifdef DFK_EXP_TABFIX
+      const f32x4* tp4 = tch + 0 * qb;
+#else
+      const f32x4* tp4 = tch + ((long)qb * nkb + kb) * 256;
+#endif
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) t[qh][h2] = tp4[qh * 2 + h2];
+    };
+    auto nxt = [&](int q) { return q + 1 == nqb ? 0 : q + 1; };
+    // one step: query block qb against the owned key block; t holds the block's table tile on entry and
+    // receives the tile of the block three steps ahead (loaded once the scores have left it)
+    auto step = [&](f32x4 (&t)[2][2], int qb) {
+      const int qr0 = qb * 32;
+      f32x4 L2[2], DL[2];
+      bf16x8 qa[2][HD / 32], da[2][HD / 32];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        const int r0 = qr0 + qh * 16 + grp * 4;
+        L2[qh] = *reinterpret_cast<const f32x4*>(lse2 + r0);
+        DL[qh] = *reinterpret_cast<const f32x4*>(delta + r0);
+#pragma unroll
+        for (int es = 0; es < HD / 32; ++es) {
+          const int off = swz<HD>(qr0 + qh * 16 + ql, es * 32 + grp * 8);
+          qa[qh][es] = *reinterpret_cast<const bf16x8*>(Qs + off);
+          da[qh][es] = *reinterpret_cast<const bf16x8*>(dOs + off);
+        }
+      }
+      // S = Q K^T (+ table), dP = dO V^T : rows = queries, lanes = keys
+      f32x4 dp[2][2];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          dp[qh][h2] = f32x4{0, 0, 0, 0};
+#pragma unroll
+          for (int es = 0; es < HD / 32; ++es) {
+            t[qh][h2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[qh][es], kB[h2][es], t[qh][h2], 0, 0, 0);
+            dp[qh][h2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[qh][es], vB[h2][es], dp[qh][h2], 0, 0, 0);
+          }
+        }
+      // P = 2^(s*scale*log2e - lse2); dS = P (dP - delta)
+      bf16x8 pa[2], sa[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float P = __builtin_amdgcn_exp2f(__builtin_fmaf(t[qh][h2][r], scale2, -L2[qh][r]));
+            float mk = 1.f;
+            if constexpr (DROP)
+              mk = drop_mul(dc, (long)blockIdx.x * Np + qr0 + qh * 16 + grp * 4 + r, kb * 32 + h2 * 16 + ql);
+            pa[h2][qh * 4 + r] = (__bf16)(P * mk);
+            sa[h2][qh * 4 + r] = (__bf16)(P * (dp[qh][h2][r] * mk - DL[qh][r]));
+          }
+      tab_tile(t, nxt(nxt(nxt(qb))));   // three steps ahead, before this step's scratch stores (vmcnt order)
+      // dS^T -> wave scratch [32 keys][32 queries] (the bf16 bits of the A operand)
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const uint4 u = __builtin_bit_cast(uint4, sa[h2]);
+        *reinterpret_cast<uint2*>(Sw + (h2 * 16 + ql) * kSdStride + grp * 4) = make_uint2(u.x, u.y);
+        *reinterpret_cast<uint2*>(Sw + (h2 * 16 + ql) * kSdStride + 16 + grp * 4) = make_uint2(u.z, u.w);
+      }
+      // dV[k][e] += P^T dO ; dK[k][e] += dS^T Q   (query slot j <-> row qr0 + (j>>2)*16 + 4grp + (j&3))
+#pragma unroll
+      for (int et = 0; et < HD / 16; ++et) {
+        const int c = et * 16 + tp * 4;
+        const int rlo = qr0 + grp * 4 + tq, rhi = rlo + 16;
+        const bf16x8 dob = tr16x2(dOs + swz<HD>(rlo, c), dOs + swz<HD>(rhi, c));
+        const bf16x8 qbv = tr16x2(Qs + swz<HD>(rlo, c), Qs + swz<HD>(rhi, c));
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          dV[h2][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[h2], dob, dV[h2][et], 0, 0, 0);
+          dK[h2][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa[h2], qbv, dK[h2][et], 0, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's own scratch writes (LDS only)
+      __builtin_amdgcn_wave_barrier();
+      // partial dQ[q][e] = dS K over this key block (dS rows via tr16 from the scratch)
+      f32x4 dq[2][HD / 16];
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        const bf16x8 sq = tr16x2(Sw + (grp * 8 + tq) * kSdStride + qh * 16 + tp * 4,
+                                 Sw + (grp * 8 + 4 + tq) * kSdStride + qh * 16 + tp * 4);
+#pragma unroll
+        for (int et = 0; et < HD / 16; ++et)
+          dq[qh][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sq, kN[et], f32x4{0, 0, 0, 0}, 0, 0, 0);
+      }
+#ifdef DFK_EXP_NODS
+      if (false) {
+#else
+      if (dsu) {   // scratch rows (32 keys x 64 B) -> global dS^T[k][q], 2 x 16 B per lane
+#endif
+        const int kr = lane >> 1, half = lane & 1;
+        const uint4 v0 = *reinterpret_cast<const uint4*>(Sw + kr * kSdStride + half * 16);
+        const uint4 v1 = *reinterpret_cast<const uint4*>(Sw + kr * kSdStride + half * 16 + 8);
+        bf16raw* gp = dsu + (long)(kb * 32 + kr) * Np + qr0 + half * 16;
+        *reinterpret_cast<uint4*>(gp) = v0;
+        *reinterpret_cast<uint4*>(gp + 8) = v1;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before the next step's writes
+      __builtin_amdgcn_wave_barrier();
+      float* acc = dQa + (size_t)qb * 32 * HD + lane * 4;
+#ifndef DFK_EXP_NOBAR
+      __syncthreads();   // every wave has finished the previous step's adds: block qb is this wave's alone
+#endif
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+        for (int et = 0; et < HD / 16; ++et) {
+          f32x4* ap = reinterpret_cast<f32x4*>(acc + (qh * (HD / 16) + et) * 256);
+          *ap = *ap + dq[qh][et];
+        }
+    };
+    f32x4 tA[2][2], tB[2][2], tC[2][2];
+    int qb = wave % nqb;   // stagger: distinct query blocks per wave at every step (nwaves <= nqb)
+    tab_tile(tA, qb);
+    tab_tile(tB, nxt(qb));
+    tab_tile(tC, nxt(nxt(qb)));
+    int i = 0;
+    for (; i + 2 < nqb; i += 3) {
+      step(tA, qb);
+      qb = nxt(qb);
+      step(tB, qb);
+      qb = nxt(qb);
+      step(tC, qb);
+      qb = nxt(qb);
+    }
+    if (i < nqb) step(tA, qb);
+    if (i + 1 < nqb) step(tB, nxt(qb));
+    // ---- dK (scaled), dV of the owned key block: C layout row = key 4grp+r, col = e
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = trow[kb * 32 + h2 * 16 + grp * 4 + r];
+#pragma unroll
+        for (int et = 0; et < HD / 16; ++et) {
+          const int e = hoff + et * 16 + ql;
+          const float vk = dK[h2][et][r] * a.scale, vv = dV[h2][et][r];
+          if (row >= 0) {
+            reinterpret_cast<bf16raw*>(ba.dk)[(long)row * ba.ld_dqkv + e] = f2bf(vk);
+            reinterpret_cast<bf16raw*>(ba.dv)[(long)row * ba.ld_dqkv + e] = f2bf(vv);
+          } else if (row == -1) {
+            if (ba.dpad_k) atomicAdd(ba.dpad_k + e, vk);
+            if (ba.dpad_v) atomicAdd(ba.dpad_v + e, vv);
+          }
+        }
+      }
+  }
+  __syncthreads();
+  // ---- dQ rows (scaled) from the accumulator: element (q, e) of block qb sits at
+  //      [qb][qh][et][lane = 16 * grp + (e & 15)][r] with q = 32 qb + 16 qh + 4 grp + r, e = 16 et + (e & 15)
+  for (int t = tid; t < Np * (HD / 8); t += blockDim.x) {
+    const int i = t / (HD / 8), c = (t % (HD / 8)) * 8;
+    const int row = i < g.N ? trow[i] : -2;
+    const int qb = i >> 5, qh = (i >> 4) & 1, gq = (i >> 2) & 3, r = i & 3, et = c >> 4;
+    const float* src = dQa + (size_t)qb * 32 * HD + (qh * (HD / 16) + et) * 256 + (gq * 16 + (c & 15)) * 4 + r;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = src[j * 4] * a.scale;
+    if (row >= 0) {
+      uint4 u;
+      bf16raw* pe = reinterpret_cast<bf16raw*>(&u);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pe[j] = f2bf(v[j]);
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16raw*>(ba.dq) + (long)row * ba.ld_dqkv + hoff + c) = u;
+    } else if (row == -1 && ba.dpad_q) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) atomicAdd(ba.dpad_q + hoff + c + j, v[j]);
+    }
+  }
+}
+
+size_t bwd_tab_lds(const dfk_wattn_args& a, const Geo& g, int nwaves) {
+  return 8 * (size_t)g.Np * a.hd + 2 * (size_t)nwaves * 32 * kSdStride + 12 * (size_t)g.Np;
+}
+
 // dRPB from the dS^T scratch: drpb[pos(q) - pos(k) + C0] += sum over windows of dS[q][k].
 // Block (chunk, head, split): 8 consecutive (k, q) elements per thread summed over the split's windows,
 // scattered into an LDS table (once per element per block), table -> one workspace row.
@@ -1746,7 +2034,27 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     const float* tabb = a.tab && !a.mask && a.scale > 0.f ? reinterpret_cast<const float*>(a.tab) + tab_elems(a, g)
                                                           : nullptr;
     if (a.drop.mode && !tabb) return DFK_EINVAL;   // attention dropout: table path only (as the forward)
-    if (a.hd == 32) PICK_B16(32); else PICK_B16(64);
+    static const int old_bwd = getenv("DFK_WATTN_BWD_OLD") ? atoi(getenv("DFK_WATTN_BWD_OLD")) : 0;
+    const size_t tlds = bwd_tab_lds(a, g, nwaves);
+    if (tabb && !old_bwd && tlds <= 160 * 1024) {
+#define LAUNCH_BT(HD, DR)                                                                              \
+  do {                                                                                                     \
+    auto kfn = wattn_bwd_tab_kernel<HD, DR>;                                                           \
+    static bool attr_set = false;                                                                          \
+    if (!attr_set) {                                                                                       \
+      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      attr_set = true;                                                                                     \
+    }                                                                                                      \
+    hipLaunchKernelGGL(kfn, dim3((unsigned)units), dim3(64 * nwaves), tlds, s, *bp, g, dsg, tabb);         \
+  } while (0)
+#define PICK_BT(HD)                                                                         \
+  do {                                                                                      \
+    if (a.drop.mode) LAUNCH_BT(HD, true); else LAUNCH_BT(HD, false);                        \
+  } while (0)
+      if (a.hd == 32) PICK_BT(32); else PICK_BT(64);
+#undef PICK_BT
+#undef LAUNCH_BT
+    } else if (a.hd == 32) PICK_B16(32); else PICK_B16(64);
 #undef PICK_B16
 #undef LAUNCH_B16
     if (want_drpb) {
