@@ -259,7 +259,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
   // register ring of PF staged k-tiles in flight (loads are unconditional: past kend they are masked
   // to zero by the view bounds), LDS double buffer: tile t is computed from LDS[t&1] while tile t+1
   // moves from its registers into LDS[(t+1)&1] and tile t+1+PF is requested into the freed registers.
-  constexpr int PF = WT == 32 ? 4 : 1;
+#ifndef DFK_GEMM_PF64
+#define DFK_GEMM_PF64 1
+#endif
+  constexpr int PF = WT == 32 ? 4 : DFK_GEMM_PF64;
   uint4 ra[PF][VA], rb[PF][VB];
   const int ntile = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
 #pragma unroll
