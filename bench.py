@@ -78,7 +78,7 @@ def time_kernel(fn, iters):
 
 
 ROOFLINE_KERNEL = "wattn_fwd_tab_kernel<32>"
-ROOFLINE_PMC = os.path.join(HERE, "profiles", "r1_wattn_fwd_pmc.json")
+ROOFLINE_PMC = os.path.join(HERE, "profiles", "r2_wattn_fwd_pmc.json")
 
 
 def roofline_case(cfg, B, dt):
