@@ -73,7 +73,8 @@ def main():
     model = build_fused(cfg, compute_dtype=dt).cuda()
     model.train()
     store = ParamStore(model, dt)
-    step = TrainStep(model, store, FusedSGD(store, 1e-4, 0.9, 1e-3), GradBucketer(store))
+    step = TrainStep(model, store, FusedSGD(store, 1e-4, 0.9, 1e-3), GradBucketer(store),
+                     parallel_branches=False)   # one stream: per-call events time only that call
     feat, label = synthetic_batch(cfg, a.batch, torch.device("cuda"), 1)
     for _ in range(2):
         step(feat, label)
