@@ -164,6 +164,35 @@ def roofline(cfg, B, dt, iters):
             "traffic_source": src, "flops_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4)}
 
 
+GEMM_KERNEL = "gemm_dma_kernel<32|64, N, N, 2>"
+
+
+def gemm_roofline(cfg, B, iters):
+    """The step's largest Linear by time on the MFMA path: Swin-T stage-3 Mlp.fc1 forward
+    (video_swin_transformer.py Mlp, src/utils.py:254-256) with its fused bias + GELU epilogue that also
+    saves the pre-activation — tokens = B * (T/2) * (H/16) * (W/16) rows, 384 -> 1536.  Algorithmic FLOPs
+    per launch = 2 * M * N * K (the epilogue's elementwise work is not counted)."""
+    from deepfake_amd import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(9)
+    M = B * (cfg["T"] // 2) * (cfg["H"] // 16) * (cfg["W"] // 16)
+    Kd, N = 384, 1536
+    x = torch.randn(M, Kd, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, Kd, device="cuda", generator=g) * Kd ** -0.5).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    aux = torch.empty_like(out)
+
+    def run():
+        K.linear(x, w, b, out=out, act=1, aux=aux)
+    t = time_kernel(run, iters)
+    flops = 2.0 * M * N * Kd
+    achieved = flops / t / 1e12
+    return {"kernel": GEMM_KERNEL + f" (Swin-T stage-3 Mlp.fc1 fwd, [{M},{Kd}]x[{Kd},{N}] + bias + GELU, pre-activation saved)",
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "flops_per_launch": flops,
+            "bytes_per_launch": (M * Kd + 2 * M * N + N * Kd) * 2, "avg_launch_ms": round(t * 1e3, 4)}
+
+
 def _cpu_train_rate(cfg_name, B, steps):
     """Median seconds per fp32 CPU train step (fwd + BCE + bwd + SGD, train-mode BatchNorm) of the oracle."""
     from oracle import fusion as OF
@@ -264,6 +293,7 @@ def main():
 
     roof = roofline(cfg, a.batch, dt, a.roofline_iters) if rank == 0 else None
     roof_conv = conv3d_roofline(cfg, a.batch, a.roofline_iters) if rank == 0 else None
+    roof_gemm = gemm_roofline(cfg, a.batch, a.roofline_iters) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
@@ -282,7 +312,7 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": not a.eager, "branch_streams": 3,
                        "regularisers": not a.deterministic, "loss": round(lossv, 5)},
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2) if train_gflop else None,
-            "roofline": roof, "roofline_conv3d": roof_conv, "cpu_baseline": cpu,
+            "roofline": roof, "roofline_conv3d": roof_conv, "roofline_gemm": roof_gemm, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -12,6 +12,9 @@
 //                            dX / dW GEMMs of every Linear never scatter.
 // LDS is double-buffered: the next tile's global loads are in flight during
 // the current tile's MFMAs, one barrier per k-tile.
+// bf16 launches with plain views take the LDS-DMA kernel instead (gemm_dma_kernel, below): the same tiles
+// and MFMAs, operands moved HBM -> LDS by buffer_load ... lds with source-swizzled, conflict-free images.
+// The register-staged kernel remains for fp32 parity mode and the implicit-conv views.
 #include "common.h"
 
 namespace {
@@ -212,6 +215,11 @@ __device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1
   }
 }
 
+template <typename T, int WT>
+__device__ __forceinline__ void tile_epilogue(const dfk_gemm_args& g, float* smem, const f32x4 (&acc)[WT / 16][WT / 16],
+                                              int lane, int wave, int bm, int bn, int z, int split, int evec,
+                                              float* slab);
+
 template <typename T, int WT, bool AK, bool BKM, bool VECOK, bool CONV, bool RS = false>
 __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int evec, float* slab) {
   constexpr int BM = 2 * WT, BN = 2 * WT, MI = WT / 16;
@@ -345,11 +353,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
         if (row < g.M) atomicAdd(g.rowsum + row, accr[mi][r]);
       }
   }
-  // ---- epilogue: stage each wave's 64x64 fp32 tile through LDS (the 16x16 MFMA C/D
-  // layout is col = lane&15, row = (lane>>4)*4 + r), then every lane owns 8
-  // consecutive columns of a row: 16-B loads of bias/residual/aux and 16-B stores.
   __syncthreads();   // every wave is done reading the last k-tile before the staging overwrites it
-  float* es = reinterpret_cast<float*>(smem) + wave * WT * ES;
+  tile_epilogue<T, WT>(g, reinterpret_cast<float*>(smem), acc, lane, wave, bm, bn, z, split, evec, slab);
+}
+
+// Epilogue shared by the GEMM kernels: stage each wave's WT x WT fp32 tile through LDS (the 16x16 MFMA C/D
+// layout is col = lane&15, row = (lane>>4)*4 + r), then every lane owns 8 consecutive columns of a row:
+// 16-B loads of bias/residual/aux and 16-B stores.  The caller has passed a barrier after its last LDS read.
+template <typename T, int WT>
+__device__ __forceinline__ void tile_epilogue(const dfk_gemm_args& g, float* smem, const f32x4 (&acc)[WT / 16][WT / 16],
+                                              int lane, int wave, int bm, int bn, int z, int split, int evec,
+                                              float* slab) {
+  constexpr int MI = WT / 16, ES = WT + 4;   // staging row stride (fp32)
+  const int wm = wave >> 1, wn = wave & 1;
+  const int z0 = z / g.nz1, z1 = z % g.nz1;
+  float* es = smem + wave * WT * ES;
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -404,6 +422,208 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
     *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(es + rl * ES + c8 + 4);
     epilogue8<T>(g, z0, z1, row, col0, v, evec);
   }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// LDS-DMA GEMM (bf16, plain views, 16-B aligned extents): the operand tiles go HBM -> LDS by
+// buffer_load_dwordx4 ... lds (16 B per lane, lane-linear 1 KB per wave-instruction) with no VGPR
+// staging and no ds_write pass — on gfx950 the register-staged ds_write_b128 (~79 B/clk/CU) costs more
+// LDS cycles per k-tile than the fragment reads, so the register-staged kernel above is LDS-bound
+// before it is MFMA-bound.  The swizzle lives on the SOURCE address (the LDS image stays lane-linear):
+//   k-contiguous operand: image [ROWS][64] (128-B rows), 16-B chunk c of row r stored at c ^ ((r>>1)&7)
+//                         -> the ds_read_b128 fragment reads are conflict-free;
+//   k-major operand     : image [64][ROWS] (k rows), chunk c of k-row k stored at c ^ kmaj_swz(k)
+//                         -> the ds_read_b64_tr_b16 transposed reads are conflict-free
+// (screened against the LDS lane-group/bank model of the microarchitecture guide).  Out-of-range chunks
+// (rows past M/N, k past the split's end) get a voffset past the descriptor's range: the hardware
+// returns zeros, so the loop has no branches around loads.  S LDS stages: tile t+S-1 is requested
+// right after the barrier that retires tile t, one raw s_barrier per k-tile, counted vmcnt waits
+// (an LDS-DMA is a VM-counter load; __syncthreads() would drain it with vmcnt(0)).
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int ROWS>
+__device__ __forceinline__ int kmaj_swz(int k) {   // 16-B chunk XOR of k-row k in a [64][ROWS] bf16 image
+  if constexpr (ROWS == 128) return ((k & 3) | ((k >> 1) & 4)) << 1;
+  else return (((k >> 1) & 1) | ((k >> 2) & 2)) << 1;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+// one operand's per-lane DMA plan: NI wave-instructions per k-tile
+template <bool KM, int ROWS>
+struct DmaPlan {
+  static constexpr int NI = ROWS / 32;          // ROWS x 64 bf16 = ROWS/8 KB per tile, 4 waves
+  uint32_t base[NI];                            // byte offset of the lane's chunk at k0 = 0
+  int kk[NI];                                   // k (within the tile) the chunk belongs to
+  bool ok[NI];                                  // row (or column chunk) inside the view
+  __device__ __forceinline__ void init(const dfk_view& v, int row0, int rowlim, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int s = (wave * NI + i) * 64 + lane;   // 16-B slot of the tile image
+      if constexpr (!KM) {
+        const int r = s >> 3, c = (s & 7) ^ ((r >> 1) & 7);
+        base[i] = (uint32_t)(((long)(row0 + r) * v.ld + c * 8) * 2);
+        kk[i] = c * 8;
+        ok[i] = row0 + r < rowlim;
+      } else {
+        constexpr int CPR = ROWS / 8;
+        const int k = s / CPR, c = (s % CPR) ^ kmaj_swz<ROWS>(k);
+        base[i] = (uint32_t)(((long)k * v.ld + row0 + c * 8) * 2);
+        kk[i] = k;
+        ok[i] = row0 + c * 8 < rowlim;
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, const dfk_view& v, int k0, int kend,
+                                        bf16raw* img, int wave) const {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const bool in = ok[i] && k0 + kk[i] < kend;
+      const uint32_t adv = KM ? (uint32_t)((long)k0 * v.ld * 2) : (uint32_t)(k0 * 2);
+      const uint32_t off = in ? base[i] + adv : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + (wave * NI + i) * 512), 16, off, 0, 0, 0);
+    }
+  }
+};
+
+// MFMA fragment (8 consecutive k of tile row r0 + (lane&15)) from a DMA-filled image
+template <bool KM, int ROWS>
+__device__ __forceinline__ bf16x8 frag_dma(const bf16raw* img, int r0, int kb, int lane) {
+  if constexpr (!KM) {
+    const int r = r0 + (lane & 15), c = (kb >> 3) + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + r * 64 + ((c ^ ((r >> 1) & 7)) << 3));
+  } else {
+    const int li = lane & 15, q = li >> 2, p = li & 3;
+    const int k = kb + (lane >> 4) * 8 + q, c = (r0 >> 3) + (p >> 1);
+    const bf16raw* lo = img + k * ROWS + ((c ^ kmaj_swz<ROWS>(k)) << 3) + (p & 1) * 4;
+    const bf16raw* hi = img + (k + 4) * ROWS + ((c ^ kmaj_swz<ROWS>(k + 4)) << 3) + (p & 1) * 4;
+    const short4v a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(lo));
+    const short4v b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(hi));
+    short8 u = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(bf16x8, u);
+  }
+}
+
+__device__ __forceinline__ uint32_t view_bytes(const dfk_view& v, long rows, long cols) {
+  return (uint32_t)(((rows - 1) * v.ld + cols) * 2);
+}
+
+template <int WT, bool AK, bool BKM, int S, bool RS>
+__global__ __launch_bounds__(256) void gemm_dma_kernel(const dfk_gemm_args g, int kchunk, int evec, float* slab) {
+  constexpr int BM = 2 * WT, BN = 2 * WT, MI = WT / 16, BK = 64;
+  constexpr int STAGE = (BM + BN) * BK;                         // elements per LDS stage
+  constexpr int ES = WT + 4;
+  constexpr int SMEM = S * STAGE * 2 > 4 * WT * ES * 4 ? S * STAGE * 2 : 4 * WT * ES * 4;   // bytes
+  constexpr int LPT = DmaPlan<AK, BM>::NI + DmaPlan<BKM, BN>::NI;   // DMA instructions per wave per tile
+  __shared__ __attribute__((aligned(16))) float smem_f[SMEM / 4];   // the ONE LDS object (staging + epilogue)
+  bf16raw* smem = reinterpret_cast<bf16raw*>(smem_f);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int tn, tmi;
+  {
+    const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    const int nid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    tn = nid % gridDim.x;
+    tmi = nid / gridDim.x;
+  }
+  const int bn = tn * BN, bm = tmi * BM;
+  int z = blockIdx.z;
+  const int split = z % g.splitk;
+  z /= g.splitk;
+  const int z0 = z / g.nz1, z1 = z % g.nz1;
+  const bf16raw* A = reinterpret_cast<const bf16raw*>(g.a.ptr) + z0 * g.a.bs0 + z1 * g.a.bs1;
+  const bf16raw* B = reinterpret_cast<const bf16raw*>(g.b.ptr) + z0 * g.b.bs0 + z1 * g.b.bs1;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16raw*>(A), (short)0, (int)(AK ? view_bytes(g.a, g.K, g.M) : view_bytes(g.a, g.M, g.K)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16raw*>(B), (short)0, (int)(BKM ? view_bytes(g.b, g.K, g.N) : view_bytes(g.b, g.N, g.K)), 0x00020000);
+  const int kbeg = split * kchunk;
+  const int kend = min(g.K, kbeg + kchunk);
+  const int ntile = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  DmaPlan<AK, BM> pa;
+  DmaPlan<BKM, BN> pb;
+  pa.init(g.a, bm, g.M, wave, lane);
+  pb.init(g.b, bn, g.N, wave, lane);
+
+  f32x4 acc[MI][MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_rs = RS && tn == 0 && wn == 0;
+  f32x4 accr[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) accr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int d = 0; d < S - 1; ++d)
+    if (d < ntile) {
+      bf16raw* st = smem + d * STAGE;
+      pa.issue(ra, g.a, kbeg + d * BK, kend, st, wave);
+      pb.issue(rb, g.b, kbeg + d * BK, kend, st + BM * BK, wave);
+    }
+  for (int t = 0; t < ntile; ++t) {
+    // retire tile t: S-2 later tiles may stay in flight (fewer near the end)
+    if constexpr (S == 4) {
+      if (t + 2 < ntile) wait_vm<2 * LPT>(); else if (t + 1 < ntile) wait_vm<LPT>(); else wait_vm<0>();
+    } else if constexpr (S == 3) {
+      if (t + 1 < ntile) wait_vm<LPT>(); else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of tile t-1 are complete
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + S - 1 < ntile) {   // refill the stage every wave finished reading at t-1
+      bf16raw* st = smem + ((t + S - 1) % S) * STAGE;
+      pa.issue(ra, g.a, kbeg + (t + S - 1) * BK, kend, st, wave);
+      pb.issue(rb, g.b, kbeg + (t + S - 1) * BK, kend, st + BM * BK, wave);
+    }
+    const bf16raw* As = smem + (t % S) * STAGE;
+    const bf16raw* Bs = As + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[MI], bfr[MI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) af[mi] = frag_dma<AK, BM>(As, wm * WT + mi * 16, ks * 32, lane);
+#pragma unroll
+      for (int ni = 0; ni < MI; ++ni) bfr[ni] = frag_dma<BKM, BN>(Bs, wn * WT + ni * 16, ks * 32, lane);
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < MI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+      if (RS && do_rs) {
+        bf16x8 ones;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) accr[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], ones, accr[mi], 0, 0, 0);
+      }
+    }
+  }
+  if (RS && do_rs && (lane & 15) == 0) {
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = bm + wm * WT + mi * 16 + (lane >> 4) * 4 + r;
+        if (row < g.M) atomicAdd(g.rowsum + row, accr[mi][r]);
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  tile_epilogue<bf16raw, WT>(g, smem_f, acc, lane, wave, bm, bn, z, split, evec, slab);
 }
 
 // split-K slabs [z][split][M][N] fp32 -> sum -> epilogue (8 columns per thread)
@@ -466,6 +686,50 @@ void dispatch_wt(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float*
   }
 }
 
+template <int WT, int S>
+void dispatch_dma_s(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+  if (g.a_kmajor) {
+    if (g.b_kmajor) {
+      if (g.rowsum) hipLaunchKernelGGL((gemm_dma_kernel<WT, true, true, S, true>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+      else hipLaunchKernelGGL((gemm_dma_kernel<WT, true, true, S, false>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    }
+    else hipLaunchKernelGGL((gemm_dma_kernel<WT, true, false, S, false>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+  } else {
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_dma_kernel<WT, false, true, S, false>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_dma_kernel<WT, false, false, S, false>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+  }
+}
+
+// LDS-DMA kernel stages (tuning runs may override): 2 for both tile sizes (C2 sweep: occupancy hides the
+// DMA latency better than a deeper ring; 128x128: 69 KB -> two workgroups per CU)
+int dma_stages(int wt) {
+  static const int s64 = getenv("DFK_DMA_S64") ? atoi(getenv("DFK_DMA_S64")) : 2;
+  static const int s32 = getenv("DFK_DMA_S32") ? atoi(getenv("DFK_DMA_S32")) : 2;
+  return wt == 64 ? s64 : s32;
+}
+
+void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+  const int st = dma_stages(wt);
+  if (wt == 64) {
+    if (st == 2) dispatch_dma_s<64, 2>(g, grid, kchunk, evec, slab, s);
+    else dispatch_dma_s<64, 3>(g, grid, kchunk, evec, slab, s);
+  } else {
+    if (st == 2) dispatch_dma_s<32, 2>(g, grid, kchunk, evec, slab, s);
+    else if (st == 4) dispatch_dma_s<32, 4>(g, grid, kchunk, evec, slab, s);
+    else dispatch_dma_s<32, 3>(g, grid, kchunk, evec, slab, s);
+  }
+}
+
+// the LDS-DMA kernel addresses each operand through a buffer descriptor with 32-bit byte offsets
+bool dma_ok(const dfk_gemm_args& g) {
+  static const int off = getenv("DFK_GEMM_DMA") ? atoi(getenv("DFK_GEMM_DMA")) == 0 : 0;   // A/B runs only
+  if (off || g.dtype != DFK_BF16 || g.a.conv_cg > 0 || g.b.conv_cg > 0) return false;
+  auto ext = [](const dfk_view& v, long rows, long cols) { return ((rows - 1) * v.ld + cols) * 2; };
+  const long ea = g.a_kmajor ? ext(g.a, g.K, g.M) : ext(g.a, g.M, g.K);
+  const long eb = g.b_kmajor ? ext(g.b, g.K, g.N) : ext(g.b, g.N, g.K);
+  return ea < 0x7fffffffL && eb < 0x7fffffffL;
+}
+
 template <typename T, bool VECOK, bool CONV>
 void dispatch(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
   if (wt == 32) dispatch_wt<T, 32, VECOK, CONV>(g, grid, kchunk, evec, slab, s);
@@ -482,6 +746,9 @@ int pick_wt(const dfk_gemm_args& g) {
   // per CU) the 64x64 tiles with the k-tile ring win or tie at every K (e.g. [25088,1536]x[1536,384] 98 -> 73
   // us, [6272,3072]x[3072,768] 86 -> 77 us), above it the 128x128 tiles win
   const long tiles128 = (long)dfk_cdiv(g.N, 128) * dfk_cdiv(g.M, 128) * g.nz0 * g.nz1;
+  // LDS-DMA kernel (below): 128x128 tiles from 1024 of them (C2 sweep: [6272,768]x[768,3072] 74 -> 58 us,
+  // the M ~ 1.6k wav2vec2 / SwinV2-stage-3 shapes stay faster on 64x64 tiles)
+  if (dma_ok(g)) return tiles128 < 1024 ? 32 : 64;
   return tiles128 < 2048 ? 32 : 64;
 }
 
@@ -493,7 +760,12 @@ int auto_splitk(const dfk_gemm_args& g) {
   const int wt = pick_wt(g);
   const long tiles = (long)dfk_cdiv(g.N, 2 * wt) * dfk_cdiv(g.M, 2 * wt) * g.nz0 * g.nz1;
   if (tiles >= 384) return 1;
-  const int maxs = g.K / (2 * TBK);                 // at least two k-tiles per split
+  static const int nosplit = getenv("DFK_GEMM_NOSPLIT") ? atoi(getenv("DFK_GEMM_NOSPLIT")) : 0;   // tuning runs only
+  if (nosplit) return 1;
+  // at least 12 k-tiles per split: below that the fp32 slab round trip and the reduce launch cost more than
+  // the shorter k-loop saves (C2 sweep of the LDS-DMA kernel: K = 512-2048 run fastest unsplit, K >= 2304
+  // with 3-4 splits)
+  const int maxs = g.K / (12 * TBK);
   const int want = (int)dfk_cdiv(768, tiles);
   return std::max(1, std::min(maxs, want));
 }
@@ -538,7 +810,8 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   const bool conv = g.a.conv_cg > 0 || g.b.conv_cg > 0;
   float* slab = autos > 1 ? reinterpret_cast<float*>(g.ws) : nullptr;
   if (vec) {
-    if (conv) dispatch<T, true, true>(gg, wt, grid, kchunk, evec, slab, s);
+    if (sizeof(T) == 2 && !conv && dma_ok(g)) dispatch_dma(gg, wt, grid, kchunk, evec, slab, s);
+    else if (conv) dispatch<T, true, true>(gg, wt, grid, kchunk, evec, slab, s);
     else dispatch<T, true, false>(gg, wt, grid, kchunk, evec, slab, s);
   } else {
     dispatch<T, false, true>(gg, wt, grid, kchunk, evec, slab, s);

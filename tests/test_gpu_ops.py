@@ -22,7 +22,8 @@ def tol(dt):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,Kd", [(1000, 288, 96), (257, 96, 384), (64, 1536, 512), (3, 512, 1024),
-                                    (1568, 512, 2048), (1592, 768, 3072)])   # last two: automatic split-K slabs
+                                    (1568, 512, 2048), (1592, 768, 3072),   # automatic split-K slabs
+                                    (8200, 4104, 200)])   # 128x128 tiles, ragged M/N, K tail inside a k-tile
 def test_linear_fwd_bwd(dt, M, N, Kd):
     g = torch.Generator(device=DEV).manual_seed(0)
     x = torch.randn(M, Kd, device=DEV, generator=g).to(dt)

@@ -21,13 +21,25 @@ SHAPES = [  # (name, M tokens, N out, K in)
 
 
 def t(fn, it=10):
+    """Per-call GPU time: `it` calls captured in one HIP graph and replayed (no host launch gaps between them)."""
     fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(it):
-        fn()
-    e.record()
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(it):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        s.record()
+        g.replay()
+        e.record()
+    except Exception:   # not capturable: eager calls
+        s.record()
+        for _ in range(it):
+            fn()
+        e.record()
     e.synchronize()
     return s.elapsed_time(e) / it / 1e3
 
@@ -36,10 +48,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--torch", action="store_true", help="also time torch (hipBLASLt) for reference")
+    ap.add_argument("--only", default="", help="comma-separated shape-name prefixes")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     tot = {"fwd": 0.0, "dx": 0.0, "dw": 0.0}
     for name, M, N, Kd in SHAPES:
+        if a.only and not any(name.startswith(p) for p in a.only.split(",")):
+            continue
         x = torch.randn(M, Kd, device="cuda").to(dt)
         w = torch.randn(N, Kd, device="cuda").to(dt)
         dy = torch.randn(M, N, device="cuda").to(dt)
