@@ -163,19 +163,21 @@ __device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1
   const long coff = z0 * g.cbs0 + z1 * g.cbs1;
   T* aux = g.aux ? reinterpret_cast<T*>(g.aux) + coff : nullptr;
   const bool full = evec && col0 + 8 <= g.N;
+  // partial groups loop over all 8 slots with a predicate: a loop bounded by ncol would index v[] dynamically
+  // and demote it (for every epilogue, full-vector path included) to scratch / LDS
   const int ncol = min(8, g.N - col0);
   if (bias) {
     if (full) { float b8[8]; ld8<T>(bias + col0, b8); for (int e = 0; e < 8; ++e) v[e] += b8[e]; }
-    else for (int e = 0; e < ncol; ++e) v[e] += ldf<T>(bias + col0 + e);
+    else for (int e = 0; e < 8; ++e) if (e < ncol) v[e] += ldf<T>(bias + col0 + e);
   }
   if (g.act == 1) {
     T* ap = aux ? aux + (long)row * g.ldaux + col0 : nullptr;
-    if (ap) { if (full) st8<T>(ap, v); else for (int e = 0; e < ncol; ++e) stf<T>(ap + e, v[e]); }
+    if (ap) { if (full) st8<T>(ap, v); else for (int e = 0; e < 8; ++e) if (e < ncol) stf<T>(ap + e, v[e]); }
     for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
   } else if (g.act == 2) {
     const T* ap = aux + (long)row * g.ldaux + col0;
     float a8[8];
-    if (full) ld8<T>(ap, a8); else for (int e = 0; e < ncol; ++e) a8[e] = ldf<T>(ap + e);
+    if (full) ld8<T>(ap, a8); else for (int e = 0; e < 8; ++e) if (e < ncol) a8[e] = ldf<T>(ap + e);
     for (int e = 0; e < 8; ++e) v[e] *= dgelu_f(a8[e]);
   }
   if (g.drop.mode && g.drop.rng) {   // dropout / DropPath of the branch output (before the residual add)
@@ -193,32 +195,32 @@ __device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1
   if (res) {
     const T* rp = res + (long)row * g.ldr + col0;
     if (full) { float r8[8]; ld8<T>(rp, r8); for (int e = 0; e < 8; ++e) v[e] += r8[e]; }
-    else for (int e = 0; e < ncol; ++e) v[e] += ldf<T>(rp + e);
+    else for (int e = 0; e < 8; ++e) if (e < ncol) v[e] += ldf<T>(rp + e);
   }
   if (g.act == 3)   // ReLU after the residual add
     for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
   const long ci = coff + (long)row * g.ldc + col0;
   if (g.atomic) {
     float* C = reinterpret_cast<float*>(g.c) + ci;
-    for (int e = 0; e < ncol; ++e) atomicAdd(C + e, v[e]);
+    for (int e = 0; e < 8; ++e) if (e < ncol) atomicAdd(C + e, v[e]);
   } else if (g.c_f32) {
     float* C = reinterpret_cast<float*>(g.c) + ci;
-    for (int e = 0; e < ncol; ++e) C[e] = g.beta != 0.f ? v[e] + g.beta * C[e] : v[e];
+    for (int e = 0; e < 8; ++e) if (e < ncol) C[e] = g.beta != 0.f ? v[e] + g.beta * C[e] : v[e];
   } else {
     T* C = reinterpret_cast<T*>(g.c) + ci;
     if (g.beta != 0.f) {
       if (full) { float c8v[8]; ld8<T>(C, c8v); for (int e = 0; e < 8; ++e) v[e] += g.beta * c8v[e]; }
-      else for (int e = 0; e < ncol; ++e) v[e] += g.beta * ldf<T>(C + e);
+      else for (int e = 0; e < 8; ++e) if (e < ncol) v[e] += g.beta * ldf<T>(C + e);
     }
     if (full) st8<T>(C, v);
-    else for (int e = 0; e < ncol; ++e) stf<T>(C + e, v[e]);
+    else for (int e = 0; e < 8; ++e) if (e < ncol) stf<T>(C + e, v[e]);
   }
 }
 
 template <typename T, int WT>
 __device__ __forceinline__ void tile_epilogue(const dfk_gemm_args& g, float* smem, const f32x4 (&acc)[WT / 16][WT / 16],
-                                              int lane, int wave, int bm, int bn, int z, int split, int evec,
-                                              float* slab);
+                                              int lane, int wave, int wm, int wn, int bm, int bn, int z, int split,
+                                              int evec, float* slab);
 
 template <typename T, int WT, bool AK, bool BKM, bool VECOK, bool CONV, bool RS = false>
 __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int evec, float* slab) {
@@ -354,7 +356,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
       }
   }
   __syncthreads();   // every wave is done reading the last k-tile before the staging overwrites it
-  tile_epilogue<T, WT>(g, reinterpret_cast<float*>(smem), acc, lane, wave, bm, bn, z, split, evec, slab);
+  tile_epilogue<T, WT>(g, reinterpret_cast<float*>(smem), acc, lane, wave, wm, wn, bm, bn, z, split, evec, slab);
 }
 
 // Epilogue shared by the GEMM kernels: stage each wave's WT x WT fp32 tile through LDS (the 16x16 MFMA C/D
@@ -362,10 +364,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
 // 16-B loads of bias/residual/aux and 16-B stores.  The caller has passed a barrier after its last LDS read.
 template <typename T, int WT>
 __device__ __forceinline__ void tile_epilogue(const dfk_gemm_args& g, float* smem, const f32x4 (&acc)[WT / 16][WT / 16],
-                                              int lane, int wave, int bm, int bn, int z, int split, int evec,
-                                              float* slab) {
+                                              int lane, int wave, int wm, int wn, int bm, int bn, int z, int split,
+                                              int evec, float* slab) {
   constexpr int MI = WT / 16, ES = WT + 4;   // staging row stride (fp32)
-  const int wm = wave >> 1, wn = wave & 1;
   const int z0 = z / g.nz1, z1 = z % g.nz1;
   float* es = smem + wave * WT * ES;
 #pragma unroll
@@ -443,52 +444,42 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 template <int ROWS>
 __device__ __forceinline__ int kmaj_swz(int k) {   // 16-B chunk XOR of k-row k in a [64][ROWS] bf16 image
-  if constexpr (ROWS == 128) return ((k & 3) | ((k >> 1) & 4)) << 1;
+  // (ROWS = 256: a k-row spans two bank rows; the XOR stays below 16, the same bank pattern as 128)
+  if constexpr (ROWS >= 128) return ((k & 3) | ((k >> 1) & 4)) << 1;
   else return (((k >> 1) & 1) | ((k >> 2) & 2)) << 1;
 }
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else static_assert(N < 0, "unsupported vmcnt");
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
 }
 
-// one operand's per-lane DMA plan: NI wave-instructions per k-tile
-template <bool KM, int ROWS>
-struct DmaPlan {
-  static constexpr int NI = ROWS / 32;          // ROWS x 64 bf16 = ROWS/8 KB per tile, 4 waves
-  uint32_t base[NI];                            // byte offset of the lane's chunk at k0 = 0
-  int kk[NI];                                   // k (within the tile) the chunk belongs to
-  bool ok[NI];                                  // row (or column chunk) inside the view
-  __device__ __forceinline__ void init(const dfk_view& v, int row0, int rowlim, int wave, int lane) {
+// One operand's DMA for k-tile k0: NI wave-instructions per wave, each 64 lanes x 16 B into 1 KB of the
+// image.  Offsets are recomputed per call in 32-bit arithmetic (the host keeps every operand below 2 GB):
+// per-lane arrays of them were demoted to scratch / LDS by the compiler.
+template <bool KM, int ROWS, int NWV>
+struct Dma {
+  static constexpr int NI = ROWS / (8 * NWV);   // ROWS x 64 bf16 = ROWS/8 KB per tile over NWV waves
+  __device__ static __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, uint32_t ld, int row0, int rowlim, int k0,
+                                               int kend, bf16raw* img, int wave, int lane) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int s = (wave * NI + i) * 64 + lane;   // 16-B slot of the tile image
+      const int sl = (wave * NI + i) * 64 + lane;   // 16-B slot of the tile image
+      uint32_t off;
+      bool in;
       if constexpr (!KM) {
-        const int r = s >> 3, c = (s & 7) ^ ((r >> 1) & 7);
-        base[i] = (uint32_t)(((long)(row0 + r) * v.ld + c * 8) * 2);
-        kk[i] = c * 8;
-        ok[i] = row0 + r < rowlim;
+        const int r = sl >> 3, c = (sl & 7) ^ ((r >> 1) & 7);
+        in = row0 + r < rowlim && k0 + c * 8 < kend;
+        off = ((uint32_t)(row0 + r) * ld + (uint32_t)(k0 + c * 8)) * 2u;
       } else {
         constexpr int CPR = ROWS / 8;
-        const int k = s / CPR, c = (s % CPR) ^ kmaj_swz<ROWS>(k);
-        base[i] = (uint32_t)(((long)k * v.ld + row0 + c * 8) * 2);
-        kk[i] = k;
-        ok[i] = row0 + c * 8 < rowlim;
+        const int k = sl / CPR, c = (sl % CPR) ^ kmaj_swz<ROWS>(k);
+        in = row0 + c * 8 < rowlim && k0 + k < kend;
+        off = ((uint32_t)(k0 + k) * ld + (uint32_t)(row0 + c * 8)) * 2u;
       }
-    }
-  }
-  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, const dfk_view& v, int k0, int kend,
-                                        bf16raw* img, int wave) const {
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const bool in = ok[i] && k0 + kk[i] < kend;
-      const uint32_t adv = KM ? (uint32_t)((long)k0 * v.ld * 2) : (uint32_t)(k0 * 2);
-      const uint32_t off = in ? base[i] + adv : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + (wave * NI + i) * 512), 16, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + (wave * NI + i) * 512), 16,
+                                               in ? off : 0x80000000u, 0, 0, 0);
     }
   }
 };
@@ -515,18 +506,22 @@ __device__ __forceinline__ uint32_t view_bytes(const dfk_view& v, long rows, lon
   return (uint32_t)(((rows - 1) * v.ld + cols) * 2);
 }
 
-template <int WT, bool AK, bool BKM, int S, bool RS>
-__global__ __launch_bounds__(256) void gemm_dma_kernel(const dfk_gemm_args g, int kchunk, int evec, float* slab) {
-  constexpr int BM = 2 * WT, BN = 2 * WT, MI = WT / 16, BK = 64;
+// Workgroup tile (NWM * 64/... ) = BM x BN from NWM x NWN waves of WT x WT each: 64x64 (2x2 waves of 32),
+// 128x128 (2x2 waves of 64) and 256x128 (4x2 waves of 64, 512 threads: twice the MFMA work per k-tile for
+// 1.5x the staged bytes, so one DMA in flight covers more of its latency).
+template <int WT, int NWM, int NWN, bool AK, bool BKM, int S, bool RS>
+__global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm_args g, int kchunk, int evec,
+                                                                  float* slab) {
+  constexpr int NWV = NWM * NWN, BM = NWM * WT, BN = NWN * WT, MI = WT / 16, BK = 64;
   constexpr int STAGE = (BM + BN) * BK;                         // elements per LDS stage
   constexpr int ES = WT + 4;
-  constexpr int SMEM = S * STAGE * 2 > 4 * WT * ES * 4 ? S * STAGE * 2 : 4 * WT * ES * 4;   // bytes
-  constexpr int LPT = DmaPlan<AK, BM>::NI + DmaPlan<BKM, BN>::NI;   // DMA instructions per wave per tile
+  constexpr int SMEM = S * STAGE * 2 > NWV * WT * ES * 4 ? S * STAGE * 2 : NWV * WT * ES * 4;   // bytes
+  constexpr int LPT = Dma<AK, BM, NWV>::NI + Dma<BKM, BN, NWV>::NI;   // DMA instructions per wave per tile
   __shared__ __attribute__((aligned(16))) float smem_f[SMEM / 4];   // the ONE LDS object (staging + epilogue)
   bf16raw* smem = reinterpret_cast<bf16raw*>(smem_f);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / NWN, wn = wave % NWN;
   int tn, tmi;
   {
     const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
@@ -550,10 +545,11 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const dfk_gemm_args g, in
   const int kend = min(g.K, kbeg + kchunk);
   const int ntile = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  DmaPlan<AK, BM> pa;
-  DmaPlan<BKM, BN> pb;
-  pa.init(g.a, bm, g.M, wave, lane);
-  pb.init(g.b, bn, g.N, wave, lane);
+  const uint32_t lda = (uint32_t)g.a.ld, ldb = (uint32_t)g.b.ld;
+  auto issue = [&](int kt, bf16raw* st) {
+    Dma<AK, BM, NWV>::issue(ra, lda, bm, g.M, kt, kend, st, wave, lane);
+    Dma<BKM, BN, NWV>::issue(rb, ldb, bn, g.N, kt, kend, st + BM * BK, wave, lane);
+  };
 
   f32x4 acc[MI][MI];
 #pragma unroll
@@ -568,9 +564,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const dfk_gemm_args g, in
 #pragma unroll
   for (int d = 0; d < S - 1; ++d)
     if (d < ntile) {
-      bf16raw* st = smem + d * STAGE;
-      pa.issue(ra, g.a, kbeg + d * BK, kend, st, wave);
-      pb.issue(rb, g.b, kbeg + d * BK, kend, st + BM * BK, wave);
+      issue(kbeg + d * BK, smem + d * STAGE);
     }
   for (int t = 0; t < ntile; ++t) {
     // retire tile t: S-2 later tiles may stay in flight (fewer near the end)
@@ -585,9 +579,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const dfk_gemm_args g, in
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (t + S - 1 < ntile) {   // refill the stage every wave finished reading at t-1
-      bf16raw* st = smem + ((t + S - 1) % S) * STAGE;
-      pa.issue(ra, g.a, kbeg + (t + S - 1) * BK, kend, st, wave);
-      pb.issue(rb, g.b, kbeg + (t + S - 1) * BK, kend, st + BM * BK, wave);
+      issue(kbeg + (t + S - 1) * BK, smem + ((t + S - 1) % S) * STAGE);
     }
     const bf16raw* As = smem + (t % S) * STAGE;
     const bf16raw* Bs = As + BM * BK;
@@ -623,7 +615,7 @@ __global__ __launch_bounds__(256) void gemm_dma_kernel(const dfk_gemm_args g, in
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  tile_epilogue<bf16raw, WT>(g, smem_f, acc, lane, wave, bm, bn, z, split, evec, slab);
+  tile_epilogue<bf16raw, WT>(g, smem_f, acc, lane, wave, wm, wn, bm, bn, z, split, evec, slab);
 }
 
 // split-K slabs [z][split][M][N] fp32 -> sum -> epilogue (8 columns per thread)
@@ -648,7 +640,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const dfk_gemm_args 
       v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
       v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
     } else {
-      for (int e = 0; e < ncol; ++e) v[e] += src[e];
+      for (int e = 0; e < 8; ++e) if (e < ncol) v[e] += src[e];
     }
   }
   epilogue8<T>(g, z / g.nz1, z % g.nz1, row, col0, v, evec);
@@ -686,37 +678,44 @@ void dispatch_wt(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float*
   }
 }
 
-template <int WT, int S>
+template <int WT, int NWM, int NWN, int S>
 void dispatch_dma_s(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+  const dim3 blk(NWM * NWN * 64);
   if (g.a_kmajor) {
     if (g.b_kmajor) {
-      if (g.rowsum) hipLaunchKernelGGL((gemm_dma_kernel<WT, true, true, S, true>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
-      else hipLaunchKernelGGL((gemm_dma_kernel<WT, true, true, S, false>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+      if (g.rowsum) hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, true, true, S, true>), grid, blk, 0, s, g, kchunk, evec, slab);
+      else hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, true, true, S, false>), grid, blk, 0, s, g, kchunk, evec, slab);
     }
-    else hipLaunchKernelGGL((gemm_dma_kernel<WT, true, false, S, false>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, true, false, S, false>), grid, blk, 0, s, g, kchunk, evec, slab);
   } else {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_dma_kernel<WT, false, true, S, false>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
-    else hipLaunchKernelGGL((gemm_dma_kernel<WT, false, false, S, false>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, false, true, S, false>), grid, blk, 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, false, false, S, false>), grid, blk, 0, s, g, kchunk, evec, slab);
   }
 }
 
 // LDS-DMA kernel stages (tuning runs may override): 2 for both tile sizes (C2 sweep: occupancy hides the
 // DMA latency better than a deeper ring; 128x128: 69 KB -> two workgroups per CU)
 int dma_stages(int wt) {
+  static const int s128 = getenv("DFK_DMA_S128") ? atoi(getenv("DFK_DMA_S128")) : 2;
+  if (wt == 128) return s128;
   static const int s64 = getenv("DFK_DMA_S64") ? atoi(getenv("DFK_DMA_S64")) : 2;
   static const int s32 = getenv("DFK_DMA_S32") ? atoi(getenv("DFK_DMA_S32")) : 2;
   return wt == 64 ? s64 : s32;
 }
 
+// wt: 32 -> 64x64 tiles, 64 -> 128x128, 128 -> 256x128 (8 waves)
 void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
   const int st = dma_stages(wt);
-  if (wt == 64) {
-    if (st == 2) dispatch_dma_s<64, 2>(g, grid, kchunk, evec, slab, s);
-    else dispatch_dma_s<64, 3>(g, grid, kchunk, evec, slab, s);
+  if (wt == 128) {
+    if (st == 3) dispatch_dma_s<64, 4, 2, 3>(g, grid, kchunk, evec, slab, s);
+    else dispatch_dma_s<64, 4, 2, 2>(g, grid, kchunk, evec, slab, s);
+  } else if (wt == 64) {
+    if (st == 2) dispatch_dma_s<64, 2, 2, 2>(g, grid, kchunk, evec, slab, s);
+    else dispatch_dma_s<64, 2, 2, 3>(g, grid, kchunk, evec, slab, s);
   } else {
-    if (st == 2) dispatch_dma_s<32, 2>(g, grid, kchunk, evec, slab, s);
-    else if (st == 4) dispatch_dma_s<32, 4>(g, grid, kchunk, evec, slab, s);
-    else dispatch_dma_s<32, 3>(g, grid, kchunk, evec, slab, s);
+    if (st == 2) dispatch_dma_s<32, 2, 2, 2>(g, grid, kchunk, evec, slab, s);
+    else if (st == 4) dispatch_dma_s<32, 2, 2, 4>(g, grid, kchunk, evec, slab, s);
+    else dispatch_dma_s<32, 2, 2, 3>(g, grid, kchunk, evec, slab, s);
   }
 }
 
@@ -796,8 +795,14 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   if (autos > 1) gg.splitk = autos;
   int kchunk = dfk_cdiv(g.K, gg.splitk);
   kchunk = dfk_cdiv(kchunk, TBK) * TBK;
-  const int wt = pick_wt(g);
-  dim3 grid(dfk_cdiv(g.N, 2 * wt), dfk_cdiv(g.M, 2 * wt), g.nz0 * g.nz1 * gg.splitk);
+  int wt = pick_wt(g);
+  const bool dma = sizeof(T) == 2 && dma_ok(g);
+  if (dma && wt == 64) {   // 256x128 tiles (8 waves) when the grid still covers the chip (tuning knob for now)
+    static const long t256 = getenv("DFK_GEMM_T256") ? atol(getenv("DFK_GEMM_T256")) : (1L << 40);
+    const long tiles256 = (long)dfk_cdiv(g.N, 128) * dfk_cdiv(g.M, 256) * g.nz0 * g.nz1 * gg.splitk;
+    if (tiles256 >= t256) wt = 128;
+  }
+  dim3 grid(dfk_cdiv(g.N, wt == 128 ? 128 : 2 * wt), dfk_cdiv(g.M, wt == 128 ? 256 : 2 * wt), g.nz0 * g.nz1 * gg.splitk);
   if (grid.y > 65535 || grid.z > 65535) return DFK_EINVAL;
   // vector path also needs the contiguous extents to be whole vectors (else tails load element-wise)
   const bool vec = view_vec(g.a, VEC) && view_vec(g.b, VEC) && (g.a_kmajor ? g.M : g.K) % VEC == 0 &&
@@ -810,7 +815,7 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   const bool conv = g.a.conv_cg > 0 || g.b.conv_cg > 0;
   float* slab = autos > 1 ? reinterpret_cast<float*>(g.ws) : nullptr;
   if (vec) {
-    if (sizeof(T) == 2 && !conv && dma_ok(g)) dispatch_dma(gg, wt, grid, kchunk, evec, slab, s);
+    if (dma) dispatch_dma(gg, wt, grid, kchunk, evec, slab, s);
     else if (conv) dispatch<T, true, true>(gg, wt, grid, kchunk, evec, slab, s);
     else dispatch<T, true, false>(gg, wt, grid, kchunk, evec, slab, s);
   } else {
