@@ -232,15 +232,31 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
   }
 }
 
-// out[j] += sum over the slab rows of part[r][col0 + j]  (64-row chunks, one atomic per chunk and column)
-__global__ __launch_bounds__(256) void slab_colsum(const float* __restrict__ part, int rows, int ld, int col0, int cols,
-                                                   float* __restrict__ out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= cols || !out) return;
-  const int r0 = blockIdx.y * 64, r1 = min(rows, r0 + 64);
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += part[(long)r * ld + col0 + j];
-  atomicAdd(out + j, s);
+// dw[j] += sum_r part[r][j], db[j] += sum_r part[r][C + j]: one launch for both halves of the [rows][2C]
+// slab; a workgroup sums 256 slab rows of 64 columns (4 row phases x 64 coalesced columns, 8 loads in
+// flight per lane), folds the phases through LDS and adds once per column (rows/256-way atomics)
+__global__ __launch_bounds__(256) void slab_colsum(const float* __restrict__ part, int rows, int C,
+                                                   float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * 256;
+  const bool ok = j < 2 * C;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 64; i += 8)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = r0 + ph + 4 * (i + u);
+      s[u] += (ok && r < rows) ? part[(long)r * 2 * C + j] : 0.f;
+    }
+  red[ph][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (ph == 0 && ok) {
+    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    float* out = j < C ? dw : db;
+    if (out) atomicAdd(out + (j < C ? j : j - C), t);
+  }
 }
 
 long bwd_blocks(long rows, int C) {
@@ -264,11 +280,9 @@ void bwd_launch(const void* dy, const void* x, const void* w, const float* mean,
   float* part = ws && (dw || db) ? ws : nullptr;
   hipLaunchKernelGGL((ln_bwd<T, L, V>), dim3(blocks), dim3(256), 2 * C * sizeof(float), s, (const T*)dy,
                      (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part, drop);
-  if (part) {
-    const dim3 g(dfk_cdiv(C, 256), dfk_cdiv(blocks, 64));
-    hipLaunchKernelGGL(slab_colsum, g, dim3(256), 0, s, part, blocks, 2 * C, 0, C, dw);
-    hipLaunchKernelGGL(slab_colsum, g, dim3(256), 0, s, part, blocks, 2 * C, C, C, db);
-  }
+  if (part)
+    hipLaunchKernelGGL(slab_colsum, dim3(dfk_cdiv(2 * C, 64), dfk_cdiv(blocks, 256)), dim3(256), 0, s, part, blocks, C,
+                       dw, db);
 }
 
 // (L, V) for C: L = lanes per row, V = 8-channel vectors per lane

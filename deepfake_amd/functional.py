@@ -207,13 +207,25 @@ def linear_group(x, weights, biases=None):
     return linear(x, W, b)
 
 
+def _skip_grad_buffer(dskip, like):
+    """The skip path's gradient as a buffer the LN backward may accumulate into in place: autograd hands a
+    Function its grad_output and forgets it once the Function returns, so the residual gradient one Function
+    passes on can carry the next one's sum."""
+    if dskip.dtype == like.dtype and dskip.is_contiguous() and dskip._base is None and dskip.shape == like.shape:
+        return dskip
+    return dskip.to(like.dtype).contiguous().reshape(like.shape).clone()
+
+
 class MlpFn(torch.autograd.Function):
     """residual + drop_out(fc2(drop_act(gelu(fc1(x))))) — src/utils.py:242-260 Mlp / HF Wav2Vec2FeedForward
     (:551-573: activation dropout after the GELU, hidden dropout after fc2) fused with the block residual
-    (video_swin_transformer.py:276: DropPath of the branch = drop_out in group mode)."""
+    (video_swin_transformer.py:276: DropPath of the branch = drop_out in group mode).
+    Skip forms (no autograd add of two gradients of one tensor): res_is_input — the residual IS x (wav2vec2's
+    x + FF(x), HF :587): dx = dpre W1 + dy in one GEMM epilogue; skip — a second output aliasing x for the
+    block's other consumer of x (SwinV2's post-norm residual): its gradient is added in the same epilogue."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, residual, drop_act=None, drop_out=None):
+    def forward(ctx, x, w1, b1, w2, b2, residual, drop_act=None, drop_out=None, res_is_input=False, skip=False):
         dt = x.dtype
         W1, B1, W2, B2 = (compute_weight(t, dt) for t in (w1, b1, w2, b2))
         pre = torch.empty(x.shape[0], w1.shape[0], device=x.device, dtype=dt)
@@ -223,10 +235,13 @@ class MlpFn(torch.autograd.Function):
             grad_use(ctx, 1 + i, p)
         ctx.save_for_backward(x, w1, b1, w2, b2, pre, h)
         ctx.has_res, ctx.drop_act, ctx.drop_out = residual is not None, drop_act, drop_out
+        ctx.res_is_input, ctx.skip = res_is_input, skip
+        if skip:
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dskip=None):
         x, w1, b1, w2, b2, pre, h = ctx.saved_tensors
         dy = dy.contiguous()
         dyr = dy
@@ -237,18 +252,27 @@ class MlpFn(torch.autograd.Function):
         db2 = grad_sink(b2)
         dw2 = grad_done(w2, K.linear_dw(dy, h, grad_sink(w2), db=db2))
         db2 = grad_done(b2, db2)
-        dx = K.linear_dx(dpre, compute_weight(w1, dt)) if ctx.needs_input_grad[0] else None
+        extra = dyr if ctx.res_is_input else (dskip if ctx.skip else None)
+        dx = K.linear_dx(dpre, compute_weight(w1, dt), residual=extra) if ctx.needs_input_grad[0] else None
         db1 = grad_sink(b1)
         dw1 = grad_done(w1, K.linear_dw(dpre, x, grad_sink(w1), db=db1))
         db1 = grad_done(b1, db1)
-        return dx, dw1, db1, dw2, db2, (dyr if ctx.has_res else None), None, None
+        dres = dyr if (ctx.has_res and not ctx.res_is_input) else None
+        return dx, dw1, db1, dw2, db2, dres, None, None, None, None
 
 
-def mlp(x, fc1, fc2, residual=None, drop_act=None, drop_out=None):
+def mlp(x, fc1, fc2, residual=None, drop_act=None, drop_out=None, skip=False):
+    """Mlp(x) (+ residual).  skip=True also returns an alias of x for the block's other consumer of x, whose
+    gradient then joins dx inside the fc1 dX GEMM."""
     shp = x.shape
-    y = MlpFn.apply(rows2d(x).contiguous(), fc1.weight, fc1.bias, fc2.weight, fc2.bias,
-                    rows2d(residual).contiguous() if residual is not None else None, drop_act, drop_out)
-    return y.view(*shp[:-1], fc2.weight.shape[0])
+    x2 = rows2d(x).contiguous()
+    res_is_input = residual is not None and residual is x
+    r2 = x2 if res_is_input else (rows2d(residual).contiguous() if residual is not None else None)
+    out = MlpFn.apply(x2, fc1.weight, fc1.bias, fc2.weight, fc2.bias, r2, drop_act, drop_out, res_is_input, skip)
+    if skip:
+        y, xs = out
+        return y.view(*shp[:-1], fc2.weight.shape[0]), xs.view(shp)
+    return out.view(*shp[:-1], fc2.weight.shape[0])
 
 
 class LayerNormFn(torch.autograd.Function):
@@ -256,29 +280,40 @@ class LayerNormFn(torch.autograd.Function):
     wav2vec2 LN -> dropout, HF :691-692)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, residual=None, drop=None):
+    def forward(ctx, x, weight, bias, eps, residual=None, drop=None, skip=False):
         dt = x.dtype
         y, mean, rstd = K.layernorm_fwd(x, compute_weight(weight, dt), compute_weight(bias, dt), eps,
                                         residual=residual, drop=drop)
         grad_use(ctx, 1, weight)
         grad_use(ctx, 2, bias)
         ctx.save_for_backward(x, weight, bias, mean, rstd)
-        ctx.drop, ctx.has_res = drop, residual is not None
+        ctx.drop, ctx.has_res, ctx.skip = drop, residual is not None, skip
+        if skip:
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dskip=None):
         x, weight, bias, mean, rstd = ctx.saved_tensors
         dy = dy.contiguous()
         dw, db = grad_sink(weight), grad_sink(bias)
-        dx = K.layernorm_bwd(dy, x, compute_weight(weight, x.dtype), mean, rstd, dw, db, drop=ctx.drop)
-        return dx, grad_done(weight, dw), grad_done(bias, db), None, (dy if ctx.has_res else None), None
+        if ctx.skip and dskip is not None:   # dx = LN'(dy) + the skip path's gradient, in one pass
+            dx = K.layernorm_bwd(dy, x, compute_weight(weight, x.dtype), mean, rstd, dw, db, drop=ctx.drop,
+                                 dx=_skip_grad_buffer(dskip, x), accumulate=True)
+        else:
+            dx = K.layernorm_bwd(dy, x, compute_weight(weight, x.dtype), mean, rstd, dw, db, drop=ctx.drop)
+        return dx, grad_done(weight, dw), grad_done(bias, db), None, (dy if ctx.has_res else None), None, None
 
 
-def layer_norm(x, ln, residual=None, drop=None):
+def layer_norm(x, ln, residual=None, drop=None, skip=False):
+    """LN(x) (residual + drop(LN(x))).  skip=True also returns an alias of x for the block's residual add:
+    the gradient arriving there is accumulated into the LN backward's dx instead of a separate add."""
     shp = x.shape
-    return LayerNormFn.apply(rows2d(x).contiguous(), ln.weight, ln.bias, ln.eps,
-                             rows2d(residual).contiguous() if residual is not None else None, drop).view(shp)
+    out = LayerNormFn.apply(rows2d(x).contiguous(), ln.weight, ln.bias, ln.eps,
+                            rows2d(residual).contiguous() if residual is not None else None, drop, skip)
+    if skip:
+        return out[0].view(shp), out[1].view(shp)
+    return out.view(shp)
 
 
 class WindowAttnFn(torch.autograd.Function):

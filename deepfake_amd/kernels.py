@@ -76,14 +76,18 @@ def linear(x, w, b=None, act=0, aux=None, residual=None, out=None, beta=0.0, dro
     return out
 
 
-def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None):
-    """dx[M,K] = dy[M,N] @ w[N,K]  (act=2: times gelu'(aux)) (drop: times the forward's dropout mask)."""
+def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None, residual=None):
+    """dx[M,K] = dy[M,N] @ w[N,K]  (act=2: times gelu'(aux)) (drop: times the forward's dropout mask)
+    (+ residual[M,K]: the gradient the input receives along a skip path, added in the epilogue)."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dy.device, dtype=dy.dtype)
+    if residual is not None:
+        residual = residual.contiguous()
     gemm(dy, dy.stride(0), False, w, w.stride(0), True, M, K, N, out, out.stride(0), dtype=L.dt(dy), act=act,
-         aux=aux, ldaux=aux.stride(0) if aux is not None else 0, beta=beta, drop=drop)
+         aux=aux, ldaux=aux.stride(0) if aux is not None else 0, beta=beta, drop=drop, residual=residual,
+         ldr=residual.stride(0) if residual is not None else 0)
     return out
 
 
@@ -127,10 +131,23 @@ def layernorm_fwd(x, w, b, eps=1e-5, out=None, residual=None, drop=None):
     return out, mean, rstd
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False, slab_partials=False, drop=None):
+def _ln_bwd_blocks(rows, C):
+    """Workgroups of ln_bwd (layernorm.hip bwd_blocks)."""
+    nv = C // 8
+    lanes = 16 if nv <= 16 else (32 if nv <= 32 else 64)
+    return min(2048, -(-rows // (4 * (64 // lanes))))
+
+
+def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False, slab_partials=None, drop=None):
+    """dx (+)= LN backward; dw / db (fp32) += the affine gradients.  slab_partials (default: from 64
+    workgroups up) writes each workgroup's dw/db partial to a slab summed by a column pass instead of adding
+    it atomically: hundreds of workgroups adding into the same C addresses serialise on a few L2 channels
+    (the 1568 x 512 SwinV2 / wav2vec2 LNs ran 20 us, the 401k x 96 stage-1 LN 116 us)."""
     rows, C = x.shape
     if dx is None:
         dx = torch.empty_like(x)
+    if slab_partials is None:
+        slab_partials = _ln_bwd_blocks(rows, C) >= 64
     ws = None
     if slab_partials and (dw is not None or db is not None):   # per-workgroup dw/db partials + column sums
         ws = torch.empty(max(L.lib().dfk_layernorm_bwd_workspace(rows, C) // 4, 1), device=x.device,

@@ -159,8 +159,8 @@ class SwinTransformerBlock(nn.Module):
         on = self.dp is not None and self.training
         dp = (self.dp[0].spec(L), self.dp[1].spec(L)) if on else (None, None)
         x2 = Fn.layer_norm(a, self.norm1, residual=x2, drop=dp[0])   # x + DropPath(LN(attn)) (:301)
-        m = Fn.mlp(x2, self.mlp.fc1, self.mlp.fc2)
-        x2 = Fn.layer_norm(m, self.norm2, residual=x2, drop=dp[1])   # x + DropPath(LN(mlp)) (:304)
+        m, x2s = Fn.mlp(x2, self.mlp.fc1, self.mlp.fc2, skip=True)   # x2's residual gradient joins fc1's dX
+        x2 = Fn.layer_norm(m, self.norm2, residual=x2s, drop=dp[1])   # x + DropPath(LN(mlp)) (:304)
         return x2.view(B, L, C)
 
 

@@ -136,24 +136,31 @@ class SwinTransformerBlock3D(nn.Module):
         self.norm2 = norm_layer(dim)
         self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
 
-    def forward_part1(self, x, mask_matrix=None):
-        """LN1 -> qkv -> shifted-window attention (pad/roll/partition in-kernel); returns pre-proj rows."""
-        B, D, H, W, C = x.shape
+    def _part1(self, xn, dims):
+        """qkv -> shifted-window attention (pad/roll/partition in-kernel) of LN1's output; pre-proj rows."""
+        B, D, H, W = dims
+        C = xn.shape[-1]
         ws, ss = get_window_size((D, H, W), self.window_size, self.shift_size)
-        xn = Fn.layer_norm(x, self.norm1)
         qkv = Fn.linear(xn.reshape(-1, C), self.attn.qkv.weight, self.attn.qkv.bias)
         return self.attn.core(qkv, (B, D, H, W), ws, ss)
 
+    def forward_part1(self, x, mask_matrix=None):
+        """LN1 -> qkv -> shifted-window attention; returns pre-proj rows."""
+        return self._part1(Fn.layer_norm(x, self.norm1), x.shape[:4])
+
     def _attn_branch(self, x, dp):
-        """x + DropPath(proj(W-MSA(LN1 x)))  (forward_part1 + the first residual, :266-271)."""
+        """x + DropPath(proj(W-MSA(LN1 x)))  (forward_part1 + the first residual, :266-271).  The residual
+        reads LN1's skip alias of x, so x's two gradients meet inside the LN backward."""
         B, D, H, W, C = x.shape
-        o = self.forward_part1(x)
-        return Fn.linear(o, self.attn.proj.weight, self.attn.proj.bias, residual=x.reshape(-1, C),
+        xn, xs = Fn.layer_norm(x, self.norm1, skip=True)
+        o = self._part1(xn, (B, D, H, W))
+        return Fn.linear(o, self.attn.proj.weight, self.attn.proj.bias, residual=xs.reshape(-1, C),
                          drop=dp).view(B, D, H, W, C)
 
     def _mlp_branch(self, x, dp):
         """x + DropPath(mlp(LN2 x))  (forward_part2 + the second residual, :273-276)."""
-        return Fn.mlp(Fn.layer_norm(x, self.norm2), self.mlp.fc1, self.mlp.fc2, residual=x, drop_out=dp)
+        xn, xs = Fn.layer_norm(x, self.norm2, skip=True)
+        return Fn.mlp(xn, self.mlp.fc1, self.mlp.fc2, residual=xs, drop_out=dp)
 
     def forward(self, x, mask_matrix=None):
         B, D, H, W, C = x.shape

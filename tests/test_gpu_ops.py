@@ -99,16 +99,20 @@ def test_layernorm(dt, rows, C):
     ref.backward(dy.float())
     dw = torch.zeros(C, device=DEV)
     db = torch.zeros(C, device=DEV)
-    dx = K.layernorm_bwd(dy, x, w, mean, rstd, dw, db)
+    dx = K.layernorm_bwd(dy, x, w, mean, rstd, dw, db, slab_partials=False)   # atomic dw/db
     assert rel(dx, xr.grad) < tol(dt) * 2
     assert rel(dw, wr.grad) < tol(dt)
     assert rel(db, br.grad) < tol(dt)
-    # dw/db through per-workgroup partials + column sums instead of atomics
+    # dw/db through per-workgroup partials + column sums instead of atomics; dx accumulated onto a
+    # residual-path gradient already in the output
     dw2 = torch.zeros(C, device=DEV)
     db2 = torch.zeros(C, device=DEV)
-    K.layernorm_bwd(dy, x, w, mean, rstd, dw2, db2, slab_partials=True)
+    dres = torch.randn(rows, C, device=DEV, generator=g).to(dt)
+    dx2 = dres.clone()
+    K.layernorm_bwd(dy, x, w, mean, rstd, dw2, db2, dx=dx2, accumulate=True, slab_partials=True)
     assert rel(dw2, wr.grad) < tol(dt)
     assert rel(db2, br.grad) < tol(dt)
+    assert rel(dx2, xr.grad + dres.float()) < tol(dt) * 2
 
 
 @pytest.mark.parametrize("heads,clamped", [(4, False), (32, True)])
