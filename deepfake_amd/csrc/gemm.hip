@@ -458,25 +458,37 @@ __device__ __forceinline__ void wait_vm() {
 // One operand's DMA for k-tile k0: NI wave-instructions per wave, each 64 lanes x 16 B into 1 KB of the
 // image.  Offsets are recomputed per call in 32-bit arithmetic (the host keeps every operand below 2 GB):
 // per-lane arrays of them were demoted to scratch / LDS by the compiler.
-template <bool KM, int ROWS, int NWV>
+template <bool KM, int ROWS, int NWV, bool CONV>
 struct Dma {
   static constexpr int NI = ROWS / (8 * NWV);   // ROWS x 64 bf16 = ROWS/8 KB per tile over NWV waves
-  __device__ static __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, uint32_t ld, int row0, int rowlim, int k0,
-                                               int kend, bf16raw* img, int wave, int lane) {
+  __device__ static __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, const dfk_view& v, int row0, int rowlim,
+                                               int k0, int kend, bf16raw* img, int wave, int lane) {
+    const uint32_t ld = (uint32_t)v.ld;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int sl = (wave * NI + i) * 64 + lane;   // 16-B slot of the tile image
-      uint32_t off;
+      int vr, vc;                                   // view row / first view column of the lane's 8 elements
       bool in;
       if constexpr (!KM) {
         const int r = sl >> 3, c = (sl & 7) ^ ((r >> 1) & 7);
-        in = row0 + r < rowlim && k0 + c * 8 < kend;
-        off = ((uint32_t)(row0 + r) * ld + (uint32_t)(k0 + c * 8)) * 2u;
+        vr = row0 + r;
+        vc = k0 + c * 8;
+        in = vr < rowlim && vc < kend;
       } else {
         constexpr int CPR = ROWS / 8;
         const int k = sl / CPR, c = (sl % CPR) ^ kmaj_swz<ROWS>(k);
-        in = row0 + c * 8 < rowlim && k0 + k < kend;
-        off = ((uint32_t)(k0 + k) * ld + (uint32_t)(row0 + c * 8)) * 2u;
+        vr = k0 + k;
+        vc = row0 + c * 8;
+        in = vc < rowlim && vr < kend;
+      }
+      uint32_t off = ((uint32_t)vr * ld + (uint32_t)vc) * 2u;
+      if constexpr (CONV) {   // implicit-conv view: column vc = tap * cg + channel of input row vr*stride + tap - pad
+        if (v.conv_cg > 0) {
+          const int tap = vc / v.conv_cg;
+          const int sr = vr * v.conv_stride + tap - v.conv_pad;
+          in = in && sr >= 0 && sr < v.conv_rows;
+          off = ((uint32_t)sr * ld + (uint32_t)(vc - tap * v.conv_cg)) * 2u;
+        }
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + (wave * NI + i) * 512), 16,
                                                in ? off : 0x80000000u, 0, 0, 0);
@@ -502,21 +514,23 @@ __device__ __forceinline__ bf16x8 frag_dma(const bf16raw* img, int r0, int kb, i
   }
 }
 
-__device__ __forceinline__ uint32_t view_bytes(const dfk_view& v, long rows, long cols) {
-  return (uint32_t)(((rows - 1) * v.ld + cols) * 2);
+// bytes a view can touch (the buffer descriptor's range): rows x cols, or an implicit-conv view's input rows
+__host__ __device__ __forceinline__ long view_extent(const dfk_view& v, long rows, long cols) {
+  if (v.conv_cg > 0) return ((long)(v.conv_rows - 1) * v.ld + v.conv_cg) * 2;
+  return ((rows - 1) * v.ld + cols) * 2;
 }
 
 // Workgroup tile (NWM * 64/... ) = BM x BN from NWM x NWN waves of WT x WT each: 64x64 (2x2 waves of 32),
 // 128x128 (2x2 waves of 64) and 256x128 (4x2 waves of 64, 512 threads: twice the MFMA work per k-tile for
 // 1.5x the staged bytes, so one DMA in flight covers more of its latency).
-template <int WT, int NWM, int NWN, bool AK, bool BKM, int S, bool RS>
+template <int WT, int NWM, int NWN, bool AK, bool BKM, int S, bool RS, bool CONV = false>
 __global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm_args g, int kchunk, int evec,
                                                                   float* slab) {
   constexpr int NWV = NWM * NWN, BM = NWM * WT, BN = NWN * WT, MI = WT / 16, BK = 64;
   constexpr int STAGE = (BM + BN) * BK;                         // elements per LDS stage
   constexpr int ES = WT + 4;
   constexpr int SMEM = S * STAGE * 2 > NWV * WT * ES * 4 ? S * STAGE * 2 : NWV * WT * ES * 4;   // bytes
-  constexpr int LPT = Dma<AK, BM, NWV>::NI + Dma<BKM, BN, NWV>::NI;   // DMA instructions per wave per tile
+  constexpr int LPT = Dma<AK, BM, NWV, CONV>::NI + Dma<BKM, BN, NWV, CONV>::NI;   // DMA instructions per wave per tile
   __shared__ __attribute__((aligned(16))) float smem_f[SMEM / 4];   // the ONE LDS object (staging + epilogue)
   bf16raw* smem = reinterpret_cast<bf16raw*>(smem_f);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -538,17 +552,16 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm
   const bf16raw* A = reinterpret_cast<const bf16raw*>(g.a.ptr) + z0 * g.a.bs0 + z1 * g.a.bs1;
   const bf16raw* B = reinterpret_cast<const bf16raw*>(g.b.ptr) + z0 * g.b.bs0 + z1 * g.b.bs1;
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16raw*>(A), (short)0, (int)(AK ? view_bytes(g.a, g.K, g.M) : view_bytes(g.a, g.M, g.K)), 0x00020000);
+      const_cast<bf16raw*>(A), (short)0, (int)(AK ? view_extent(g.a, g.K, g.M) : view_extent(g.a, g.M, g.K)), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16raw*>(B), (short)0, (int)(BKM ? view_bytes(g.b, g.K, g.N) : view_bytes(g.b, g.N, g.K)), 0x00020000);
+      const_cast<bf16raw*>(B), (short)0, (int)(BKM ? view_extent(g.b, g.K, g.N) : view_extent(g.b, g.N, g.K)), 0x00020000);
   const int kbeg = split * kchunk;
   const int kend = min(g.K, kbeg + kchunk);
   const int ntile = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  const uint32_t lda = (uint32_t)g.a.ld, ldb = (uint32_t)g.b.ld;
   auto issue = [&](int kt, bf16raw* st) {
-    Dma<AK, BM, NWV>::issue(ra, lda, bm, g.M, kt, kend, st, wave, lane);
-    Dma<BKM, BN, NWV>::issue(rb, ldb, bn, g.N, kt, kend, st + BM * BK, wave, lane);
+    Dma<AK, BM, NWV, CONV>::issue(ra, g.a, bm, g.M, kt, kend, st, wave, lane);
+    Dma<BKM, BN, NWV, CONV>::issue(rb, g.b, bn, g.N, kt, kend, st + BM * BK, wave, lane);
   };
 
   f32x4 acc[MI][MI];
@@ -678,6 +691,22 @@ void dispatch_wt(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float*
   }
 }
 
+// implicit-conv views (wav2vec2 conv1-6 and their weight gradients): 2 LDS stages, 64x64 / 128x128 tiles
+template <int WT>
+void dispatch_dma_conv(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+  const dim3 blk(256);
+  if (g.a_kmajor) {
+    if (g.b_kmajor) {
+      if (g.rowsum) hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, true, true, 2, true, true>), grid, blk, 0, s, g, kchunk, evec, slab);
+      else hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, true, true, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, slab);
+    }
+    else hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, true, false, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, slab);
+  } else {
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, false, true, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, false, false, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, slab);
+  }
+}
+
 template <int WT, int NWM, int NWN, int S>
 void dispatch_dma_s(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
   const dim3 blk(NWM * NWN * 64);
@@ -705,6 +734,11 @@ int dma_stages(int wt) {
 
 // wt: 32 -> 64x64 tiles, 64 -> 128x128, 128 -> 256x128 (8 waves)
 void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+  if (g.a.conv_cg > 0 || g.b.conv_cg > 0) {
+    if (wt == 32) dispatch_dma_conv<32>(g, grid, kchunk, evec, slab, s);
+    else dispatch_dma_conv<64>(g, grid, kchunk, evec, slab, s);
+    return;
+  }
   const int st = dma_stages(wt);
   if (wt == 128) {
     if (st == 3) dispatch_dma_s<64, 4, 2, 3>(g, grid, kchunk, evec, slab, s);
@@ -722,10 +756,9 @@ void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int eve
 // the LDS-DMA kernel addresses each operand through a buffer descriptor with 32-bit byte offsets
 bool dma_ok(const dfk_gemm_args& g) {
   static const int off = getenv("DFK_GEMM_DMA") ? atoi(getenv("DFK_GEMM_DMA")) == 0 : 0;   // A/B runs only
-  if (off || g.dtype != DFK_BF16 || g.a.conv_cg > 0 || g.b.conv_cg > 0) return false;
-  auto ext = [](const dfk_view& v, long rows, long cols) { return ((rows - 1) * v.ld + cols) * 2; };
-  const long ea = g.a_kmajor ? ext(g.a, g.K, g.M) : ext(g.a, g.M, g.K);
-  const long eb = g.b_kmajor ? ext(g.b, g.K, g.N) : ext(g.b, g.N, g.K);
+  if (off || g.dtype != DFK_BF16) return false;
+  const long ea = g.a_kmajor ? view_extent(g.a, g.K, g.M) : view_extent(g.a, g.M, g.K);
+  const long eb = g.b_kmajor ? view_extent(g.b, g.K, g.N) : view_extent(g.b, g.N, g.K);
   return ea < 0x7fffffffL && eb < 0x7fffffffL;
 }
 
@@ -797,7 +830,8 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   kchunk = dfk_cdiv(kchunk, TBK) * TBK;
   int wt = pick_wt(g);
   const bool dma = sizeof(T) == 2 && dma_ok(g);
-  if (dma && wt == 64) {   // 256x128 tiles (8 waves) when the grid still covers the chip (tuning knob for now)
+  const bool conv = g.a.conv_cg > 0 || g.b.conv_cg > 0;
+  if (dma && wt == 64 && !conv) {   // 256x128 tiles (8 waves) when the grid still covers the chip (tuning knob for now)
     static const long t256 = getenv("DFK_GEMM_T256") ? atol(getenv("DFK_GEMM_T256")) : (1L << 40);
     const long tiles256 = (long)dfk_cdiv(g.N, 128) * dfk_cdiv(g.M, 256) * g.nz0 * g.nz1 * gg.splitk;
     if (tiles256 >= t256) wt = 128;
@@ -812,7 +846,6 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
                     (!g.bias || (aligned16(g.bias) && g.bias_bs1 % 8 == 0)) &&
                     (!g.residual || (aligned16(g.residual) && g.ldr % 8 == 0 && g.rbs0 % 8 == 0 && g.rbs1 % 8 == 0)) &&
                     (!g.aux || (aligned16(g.aux) && g.ldaux % 8 == 0));
-  const bool conv = g.a.conv_cg > 0 || g.b.conv_cg > 0;
   float* slab = autos > 1 ? reinterpret_cast<float*>(g.ws) : nullptr;
   if (vec) {
     if (dma) dispatch_dma(gg, wt, grid, kchunk, evec, slab, s);
