@@ -211,8 +211,8 @@ def _skip_grad_buffer(dskip, like):
     """The skip path's gradient as a buffer the LN backward may accumulate into in place: autograd hands a
     Function its grad_output and forgets it once the Function returns, so the residual gradient one Function
     passes on can carry the next one's sum."""
-    if dskip.dtype == like.dtype and dskip.is_contiguous() and dskip._base is None and dskip.shape == like.shape:
-        return dskip
+    if dskip.dtype == like.dtype and dskip.is_contiguous() and dskip.numel() == like.numel():
+        return dskip.view(like.shape)   # (often a reshape view of the producer's grad_output: same memory)
     return dskip.to(like.dtype).contiguous().reshape(like.shape).clone()
 
 

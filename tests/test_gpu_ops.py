@@ -154,3 +154,51 @@ def test_cpb_bias_and_cosine_logit_scale(heads, clamped):
     yr.backward(dy)
     assert rel(x.grad, xr.grad) < 1e-4
     assert rel(logit.grad, lr.grad) < 1e-4
+
+
+@pytest.mark.parametrize("C", [96, 384])
+def test_skip_gradient_fusion(C):
+    """Skip forms of LayerNormFn / MlpFn (one backward pass adds the gradient the input receives along the
+    block's residual): a pre-norm block  y = x + mlp(LN(x))  built from the skip alias, a SwinV2-style
+    post-norm  y = LN2(mlp(x)) + x  through MlpFn's alias, and wav2vec2's  x + FF(x)  with the residual
+    being the input, each against the same graph in fp32 torch."""
+    from deepfake_amd import functional as Fn
+    torch.manual_seed(3)
+    M = 300
+    ln = torch.nn.LayerNorm(C).to(DEV)
+    fc1, fc2 = torch.nn.Linear(C, 4 * C).to(DEV), torch.nn.Linear(4 * C, C).to(DEV)
+    with torch.no_grad():
+        for p in (ln.weight, ln.bias):
+            p.add_(torch.randn_like(p) * 0.1)
+    x0 = torch.randn(M, C, device=DEV)
+    g = torch.randn(M, C, device=DEV)
+
+    def ref_mlp(t):
+        return fc2(torch.nn.functional.gelu(fc1(t)))
+
+    def grads(fn):
+        x = x0.clone().requires_grad_(True)
+        for p in (*ln.parameters(), *fc1.parameters(), *fc2.parameters()):
+            p.grad = None
+        (fn(x) * g).sum().backward()
+        return [x.grad] + [p.grad.clone() for p in (ln.weight, ln.bias, fc1.weight, fc2.weight)]
+
+    def pre_norm(x):
+        xn, xs = Fn.layer_norm(x, ln, skip=True)
+        return Fn.mlp(xn, fc1, fc2, residual=xs)
+
+    def post_norm(x):
+        m, xs = Fn.mlp(x, fc1, fc2, skip=True)
+        return Fn.layer_norm(m, ln, residual=xs)
+
+    def res_input(x):
+        return Fn.mlp(x, fc1, fc2, residual=x)
+
+    cases = [(pre_norm, lambda x: x + ref_mlp(ln(x))), (post_norm, lambda x: x + ln(ref_mlp(x))),
+             (res_input, lambda x: x + ref_mlp(x))]
+    for ours, ref in cases:
+        for a, b in zip(grads(ours), grads(ref)):
+            if b is None:
+                continue
+            assert a is not None
+            assert rel(a, b) < 1e-4
