@@ -91,7 +91,11 @@ def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None, residual=No
     return out
 
 
-def splitk_for(tiles, K, min_k=256):
+_DW_MIN_K = int(os.environ.get("DFK_DW_MINK", "256"))   # tokens per split of a weight-gradient GEMM (tuning)
+
+
+def splitk_for(tiles, K, min_k=None):
+    min_k = _DW_MIN_K if min_k is None else min_k
     return max(1, min(_CU_TARGET_BLOCKS // max(tiles, 1), max(K // min_k, 1)))
 
 
