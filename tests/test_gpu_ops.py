@@ -181,7 +181,7 @@ def test_skip_gradient_fusion(C):
         for p in (*ln.parameters(), *fc1.parameters(), *fc2.parameters()):
             p.grad = None
         (fn(x) * g).sum().backward()
-        return [x.grad] + [p.grad.clone() for p in (ln.weight, ln.bias, fc1.weight, fc2.weight)]
+        return [x.grad] + [p.grad.clone() if p.grad is not None else None for p in (ln.weight, ln.bias, fc1.weight, fc2.weight)]
 
     def pre_norm(x):
         xn, xs = Fn.layer_norm(x, ln, skip=True)
