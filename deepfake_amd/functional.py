@@ -152,7 +152,7 @@ class GroupLinearFn(torch.autograd.Function):
     writes dW / db straight into the flat gradient view, then reports every member ready."""
 
     @staticmethod
-    def forward(ctx, x, st, wspan, wshape, bspan, *params):
+    def forward(ctx, x, st, wspan, wshape, bspan, skip, *params):
         dt = x.dtype
         src = st.shadow if (dt == torch.bfloat16 and st.shadow is not None) else st.flat
         if src.dtype != dt:
@@ -161,33 +161,38 @@ class GroupLinearFn(torch.autograd.Function):
         B = src[bspan[0]:bspan[0] + bspan[1]] if bspan is not None else None
         y = K.linear(x, W, B)
         for i, p in enumerate(params):
-            grad_use(ctx, 5 + i, p)
+            grad_use(ctx, 6 + i, p)
         ctx.save_for_backward(x, *params)
-        ctx.st, ctx.wspan, ctx.wshape, ctx.bspan = st, wspan, wshape, bspan
+        ctx.st, ctx.wspan, ctx.wshape, ctx.bspan, ctx.skip = st, wspan, wshape, bspan, skip
+        if skip:
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dskip=None):
         x, *params = ctx.saved_tensors
         st, (wo, wn), wshape, bspan = ctx.st, ctx.wspan, ctx.wshape, ctx.bspan
         dy = dy.contiguous()
         src = st.shadow if (x.dtype == torch.bfloat16 and st.shadow is not None) else st.flat
-        dx = K.linear_dx(dy, src[wo:wo + wn].view(wshape)) if ctx.needs_input_grad[0] else None
+        # the skip alias's gradient (the block's residual path) joins dx in the GEMM epilogue
+        dx = K.linear_dx(dy, src[wo:wo + wn].view(wshape), residual=dskip if ctx.skip else None) \
+            if ctx.needs_input_grad[0] else None
         if any(p.grad is None for p in params):
             st.rebind_grads()
         db = st.grad[bspan[0]:bspan[0] + bspan[1]] if bspan is not None else None
         K.linear_dw(dy, x, st.grad[wo:wo + wn].view(wshape), db=db)
         for p in params:
             grad_done(p, None)
-        return (dx, None, None, None, None) + (None,) * len(params)
+        return (dx, None, None, None, None, None) + (None,) * len(params)
 
 
-def linear_group(x, weights, biases=None):
+def linear_group(x, weights, biases=None, skip=False):
     """nn.Linear over concatenated parameters: W = cat(weights) [sum N_i, K], b = cat(biases) with int
     entries of `biases` standing for zero gaps (SwinV2's qkv bias = cat(q_bias, 0, v_bias),
     swin_transformer2d.py:151-153; wav2vec2's separate q/k/v projections, HF :495-498).  With a ParamStore
     that laid the groups out adjacently (module.flat_groups()) nothing is concatenated; otherwise the
-    reference's torch.cat."""
+    reference's torch.cat.  skip=True also returns an alias of x for the block's residual consumer (its
+    gradient is added in the dX GEMM epilogue; on the torch.cat fallback the alias is x itself)."""
     shp = x.shape
     x2 = rows2d(x).contiguous()
     st = _store(weights[0])
@@ -197,14 +202,17 @@ def linear_group(x, weights, biases=None):
         if ws is not None and (biases is None or bs is not None):
             wshape = (sum(w.shape[0] for w in weights), weights[0].shape[1])
             ps = list(weights) + [b for b in (biases or []) if not isinstance(b, int)]
-            y = GroupLinearFn.apply(x2, st, ws, wshape, bs, *ps)
-            return y.view(*shp[:-1], wshape[0])
+            out = GroupLinearFn.apply(x2, st, ws, wshape, bs, skip, *ps)
+            if skip:
+                return out[0].view(*shp[:-1], wshape[0]), out[1].view(shp)
+            return out.view(*shp[:-1], wshape[0])
     W = torch.cat(list(weights)) if len(weights) > 1 else weights[0]
     b = None
     if biases is not None:
         b = torch.cat([torch.zeros(e, device=x.device, dtype=weights[0].dtype) if isinstance(e, int) else e
                        for e in biases])
-    return linear(x, W, b)
+    y = linear(x, W, b)
+    return (y, x) if skip else y
 
 
 def _skip_grad_buffer(dskip, like):

@@ -96,18 +96,23 @@ class WindowAttention(nn.Module):
         """ParamStore adjacency: q_bias, a C-element zero gap, v_bias -> the [3C] qkv bias in place."""
         return [[self.q_bias, self.dim, self.v_bias]] if self.q_bias is not None else []
 
-    def core(self, x2d, dims, ws, shift):
-        """x2d [rows, C] -> attention output [rows, C] before proj."""
+    def core(self, x2d, dims, ws, shift, skip=False):
+        """x2d [rows, C] -> attention output [rows, C] before proj (skip=True: and an alias of x2d for the
+        block's residual, whose gradient joins the qkv dX GEMM)."""
         C = self.dim
         hd = C // self.num_heads
+        xs = x2d
         if self.q_bias is not None:   # qkv bias = cat(q_bias, 0, v_bias) (:151-153): a gapped adjacency group
-            qkv = Fn.linear_group(x2d, (self.qkv.weight,), (self.q_bias, C, self.v_bias))
+            qkv = Fn.linear_group(x2d, (self.qkv.weight,), (self.q_bias, C, self.v_bias), skip=skip)
+            if skip:
+                qkv, xs = qkv
         else:
             qkv = Fn.linear(x2d, self.qkv.weight)
         qkv = Fn.CosineQKFn.apply(qkv, self.logit_scale, self.num_heads, hd, math.log(1. / 0.01))
         geo = (dims, (1, ws, ws), (1, self.window_size[0], self.window_size[1]), (0, shift, shift),
                self.num_heads, hd, 1.0)
-        return Fn.window_attention(qkv, self.bias_table(), None, geo)
+        out = Fn.window_attention(qkv, self.bias_table(), None, geo)
+        return (out, xs) if skip else out
 
 
 class SwinTransformerBlock(nn.Module):
@@ -154,11 +159,11 @@ class SwinTransformerBlock(nn.Module):
         B, L, C = x.shape
         assert L == H * W, "input feature has wrong size"
         x2 = x.reshape(-1, C)
-        a = self.attn.core(x2, (B, 1, H, W), self.window_size, self.shift_size)
+        a, x2s = self.attn.core(x2, (B, 1, H, W), self.window_size, self.shift_size, skip=True)
         a = Fn.linear(a, self.attn.proj.weight, self.attn.proj.bias)
         on = self.dp is not None and self.training
         dp = (self.dp[0].spec(L), self.dp[1].spec(L)) if on else (None, None)
-        x2 = Fn.layer_norm(a, self.norm1, residual=x2, drop=dp[0])   # x + DropPath(LN(attn)) (:301)
+        x2 = Fn.layer_norm(a, self.norm1, residual=x2s, drop=dp[0])   # x + DropPath(LN(attn)) (:301)
         m, x2s = Fn.mlp(x2, self.mlp.fc1, self.mlp.fc2, skip=True)   # x2's residual gradient joins fc1's dX
         x2 = Fn.layer_norm(m, self.norm2, residual=x2s, drop=dp[1])   # x + DropPath(LN(mlp)) (:304)
         return x2.view(B, L, C)

@@ -167,13 +167,17 @@ class Wav2Vec2Attention(nn.Module):
         q, k, v = self.q_proj, self.k_proj, self.v_proj
         return [[q.weight, k.weight, v.weight], [q.bias, k.bias, v.bias]]
 
-    def core(self, x, B, T):
-        """x [B*T, C] -> attention output [B*T, C] before out_proj."""
+    def core(self, x, B, T, skip=False):
+        """x [B*T, C] -> attention output [B*T, C] before out_proj (skip=True: and an alias of x for the
+        layer's residual, whose gradient joins the q/k/v dX GEMM)."""
         q, k, v = self.q_proj, self.k_proj, self.v_proj
-        qkv = Fn.linear_group(x, (q.weight, k.weight, v.weight), (q.bias, k.bias, v.bias))
+        qkv = Fn.linear_group(x, (q.weight, k.weight, v.weight), (q.bias, k.bias, v.bias), skip=skip)
+        if skip:
+            qkv, xs = qkv
         geo = ((B, 1, 1, T), (1, 1, T), (1, 1, T), (0, 0, 0), self.num_heads, self.head_dim, self.scaling)
         d = self.dropout.spec() if self.dropout.active(self.training) else None
-        return Fn.window_attention(qkv, None, None, geo, drop=d)
+        out = Fn.window_attention(qkv, None, None, geo, drop=d)
+        return (out, xs) if skip else out
 
 
 class Wav2Vec2FeedForward(nn.Module):
@@ -202,8 +206,8 @@ class Wav2Vec2EncoderLayer(nn.Module):
         tr = self.training
         ff = self.feed_forward
         spec = lambda d: d.spec() if d.active(tr) else None   # noqa: E731
-        a = self.attention.core(x, B, T)
-        x = Fn.layer_norm(Fn.linear(a, self.attention.out_proj.weight, self.attention.out_proj.bias, residual=x,
+        a, xs = self.attention.core(x, B, T, skip=True)
+        x = Fn.layer_norm(Fn.linear(a, self.attention.out_proj.weight, self.attention.out_proj.bias, residual=xs,
                                     drop=spec(self.dropout)), self.layer_norm)
         x = Fn.mlp(x, ff.intermediate_dense, ff.output_dense, residual=x, drop_act=spec(ff.intermediate_dropout),
                    drop_out=spec(ff.output_dropout))
