@@ -30,6 +30,12 @@ import time
 import torch
 import torch.distributed as dist
 
+# Before any process group exists: RCCL work events are not drawn from torch's event cache, so the bucket
+# all-reduces captured into the step's HIP graph never share an event with an eager collective the
+# ProcessGroupNCCL watchdog is still polling (with the cache on, the watchdog's query of a
+# capture-recorded event aborts the process: tools/ddp_graph_probe.py).
+os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 

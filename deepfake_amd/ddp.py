@@ -21,6 +21,7 @@ just accumulate in the flat buffer — and only the last micro-step's backward
 launches the bucket all-reduces, each over the sum of every micro-step.
 """
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -51,7 +52,9 @@ class GradBucketer:
                 self.bucket_of[i] = b
         self.pending = [0] * len(self.buckets)
         self.works = [None] * len(self.buckets)
-        self.enabled = self.world > 1
+        # DFK_DDP_FORCE=1 (tests / probes only): reduce even at one rank, so a 1-GPU box exercises the RCCL
+        # launches, including their capture into the step's HIP graph
+        self.enabled = self.world > 1 or (dist.is_initialized() and os.environ.get("DFK_DDP_FORCE") == "1")
         self.overlap = True       # hooks launch bucket all-reduces during backward (eager steps)
         self.sync = True          # False inside no_sync(): accumulation micro-steps launch nothing
         self.hooks = []

@@ -123,35 +123,56 @@ class TrainStep:
 
     def _capture(self, feature, label):
         """One eager step (initialises momentum, allocator warm-up), then capture the
-        whole step — grad zeroing, fwd, bwd, bucket all-reduces, SGD — as one graph."""
+        whole step — grad zeroing, fwd, bwd, bucket all-reduces, SGD — as one graph.
+        Multi-GPU: the bucket all-reduces are captured where the backward completes each bucket (on the
+        comm stream, overlapping the rest of backward, §8e); if the backend cannot capture that form the
+        capture is retried with one all-reduce pass after backward, and only then does the step stay eager."""
         loss, prob = self.eager(feature, label)
         torch.cuda.synchronize()
+        if self.bucketer.enabled:
+            # let the ProcessGroupNCCL watchdog retire the eager step's RCCL works before the capture: it polls
+            # their events, and HIP refuses an event query while that event's stream (the RCCL stream, which
+            # the captured all-reduces join) is capturing — the watchdog thread then aborts the process
+            time.sleep(1.0)
         static_in = [x.clone() for x in feature]
         static_label = label.clone()
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        self.bucketer.overlap = False
-        try:
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
-                    self.store.grad.zero_()
-                    l2, p2 = self._fwd_bwd(tuple(static_in), static_label)
-                    self.bucketer.allreduce_all()
-                    self.opt.step(first=False)
-        except RuntimeError as e:         # e.g. a collective the backend cannot capture: stay eager
-            torch.cuda.synchronize()
+        err = None
+        forms = (True, False) if self.bucketer.enabled else (False,)
+        if os.environ.get("DFK_CAPTURE_OVERLAP") == "0":   # probes: only the one-pass form
+            forms = (False,)
+        for overlap in forms:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            self.bucketer.overlap = overlap
+            self.bucketer.reset()
+            self.store.uses.clear()   # a failed attempt may have left forward-use counts behind
+            try:
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s):
+                        self.store.grad.zero_()
+                        l2, p2 = self._fwd_bwd(tuple(static_in), static_label)
+                        if overlap:
+                            self.bucketer.finish()         # flush unused buckets, join the comm stream, average
+                        else:
+                            self.bucketer.allreduce_all()
+                        self.opt.step(first=False)
+            except RuntimeError as e:         # e.g. a collective the backend cannot capture in this form
+                torch.cuda.synchronize()
+                err = e
+                continue
+            torch.cuda.current_stream().wait_stream(s)
             self.bucketer.overlap = True
             self.bucketer.reset()
-            self.graph_mode = False
-            print(f"[deepfake_amd] HIP-graph capture failed ({e}); running the step eagerly", flush=True)
-            self.store.zero_grad()
+            self.graph = g
+            self.static = (static_in, static_label, l2, p2)
+            self.captured_overlap = overlap
             return loss, prob
-        torch.cuda.current_stream().wait_stream(s)
         self.bucketer.overlap = True
         self.bucketer.reset()
-        self.graph = g
-        self.static = (static_in, static_label, l2, p2)
+        self.graph_mode = False
+        print(f"[deepfake_amd] HIP-graph capture failed ({err}); running the step eagerly", flush=True)
+        self.store.zero_grad()
         return loss, prob
 
 
