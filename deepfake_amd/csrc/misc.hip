@@ -108,14 +108,24 @@ __global__ void merge_kernel(const T* __restrict__ src, T* __restrict__ dst, int
 
 // out[g][c] = mean_r x[g*R + r][c]   (fp32 accumulation)
 template <typename T, typename TO>
-__global__ void rowmean_kernel(const T* __restrict__ x, TO* __restrict__ out, int R, int C) {
-  const int g = blockIdx.y;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const T* p = x + (long)g * R * C + c;
-  float s = 0.f;
-  for (int r = 0; r < R; ++r) s += ldf<T>(p + (long)r * C);
-  stf<TO>(out + (long)g * C + c, s / R);
+__global__ __launch_bounds__(256) void rowmean_kernel(const T* __restrict__ x, TO* __restrict__ out, int R, int C) {
+  // workgroup = (64 columns, group): 4 row phases x 64 coalesced columns, 8 independent partial sums per lane
+  // (a thread walking all R rows serially was a chain of R dependent-latency loads: 116 us at R = 784)
+  __shared__ float red[4][64];
+  const int g = blockIdx.y, lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const bool ok = c < C;
+  const T* p = x + (long)g * R * C + (ok ? c : 0);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int r = ph;
+  for (; r + 28 < R; r += 32)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += ldf<T>(p + (long)(r + 4 * u) * C);
+  for (; r < R; r += 4) s[0] += ldf<T>(p + (long)r * C);
+  red[ph][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (ph == 0 && ok)
+    stf<TO>(out + (long)g * C + c, ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane])) / R);
 }
 
 template <typename T>
@@ -362,7 +372,7 @@ extern "C" int dfk_patch_merge(const void* src, void* dst, int B, int D, int H, 
 
 extern "C" int dfk_rowmean(const void* x, void* out, int groups, int R, int C, int dtype, int out_f32, hipStream_t s) {
   if (!x || !out || R <= 0) return DFK_EINVAL;
-  const dim3 grid(dfk_cdiv(C, 256), groups);
+  const dim3 grid(dfk_cdiv(C, 64), groups);
   if (dtype == DFK_BF16) {
     if (out_f32) hipLaunchKernelGGL((rowmean_kernel<bf16raw, float>), grid, dim3(256), 0, s, (const bf16raw*)x, (float*)out, R, C);
     else hipLaunchKernelGGL((rowmean_kernel<bf16raw, bf16raw>), grid, dim3(256), 0, s, (const bf16raw*)x, (bf16raw*)out, R, C);

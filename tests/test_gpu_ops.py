@@ -202,3 +202,14 @@ def test_skip_gradient_fusion(C):
                 continue
             assert a is not None
             assert rel(a, b) < 1e-4
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("groups,R,C", [(8, 784, 768), (3, 5, 100), (2, 37, 1536), (1, 1, 64)])
+def test_rowmean(dt, groups, R, C):
+    """dfk_rowmean (VSTFeat's mean over a clip's tokens, the Inception global average pool) against torch."""
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(groups * R, C, device=DEV, generator=g).to(dt)
+    out = K.rowmean(x, groups)
+    ref = x.float().view(groups, R, C).mean(1)
+    assert rel(out, ref) < 1e-5
