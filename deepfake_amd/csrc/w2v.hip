@@ -112,9 +112,10 @@ __global__ __launch_bounds__(256) void conv0_bwd_dw(const float* __restrict__ x,
                                                     int T0, const float* __restrict__ stats,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                                     float eps, const T* __restrict__ dout, const float* __restrict__ red,
-                                                    float* __restrict__ dw) {
-  // each workgroup sweeps a strided set of time blocks and keeps its dw partials in registers, so the
-  // 5120 dw entries take one atomic per workgroup (not one per 64-step block: same-address contention)
+                                                    float* __restrict__ part) {
+  // each workgroup sweeps a strided set of time blocks and keeps its dw partials in registers, then writes
+  // them once to its slab row (four workgroups per CU: the recompute of conv + GroupNorm + GELU' is VALU work
+  // that one wave per SIMD left latency-bound)
   __shared__ float xs[TB * KS + KW];
   __shared__ float ws[CH * KW];
   const int b = blockIdx.y;
@@ -154,10 +155,33 @@ __global__ __launch_bounds__(256) void conv0_bwd_dw(const float* __restrict__ x,
       }
     }
   }
+  // this workgroup's partial -> its slab row (summed by dw_slab_sum: no same-address atomics across the
+  // workgroups of the grid)
+  float* row = part + ((long)blockIdx.y * gridDim.x + blockIdx.x) * (CH * KW);
 #pragma unroll
   for (int j = 0; j < CPT; ++j)
 #pragma unroll
-    for (int k = 0; k < KW; ++k) atomicAdd(dw + (threadIdx.x + j * 256) * KW + k, acc[j][k]);
+    for (int k = 0; k < KW; ++k) row[(threadIdx.x + j * 256) * KW + k] = acc[j][k];
+}
+
+// dw[i] += sum over the slab rows of part[r][i]  (i < CH*KW): workgroup = 64 columns x one 128-row chunk,
+// 4 row phases x 8 loads in flight per lane, one atomic per column and chunk
+__global__ __launch_bounds__(256) void dw_slab_sum(const float* __restrict__ part, int rows, float* __restrict__ dw) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * 128, r1 = min(rows, r0 + 128);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (i < CH * KW) {
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int r = r0 + ph + 4 * u;
+      if (r < r1) s[u & 7] += part[(long)r * (CH * KW) + i];
+    }
+  }
+  red[ph][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (ph == 0 && i < CH * KW) atomicAdd(dw + i, (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]));
 }
 
 // dgamma[c] += sum_b A[b,c] ; dbeta[c] += sum_b Bs[b,c]
@@ -170,7 +194,16 @@ __global__ void gn_affine_grad(const float* __restrict__ red, int B, float* dgam
   if (dbeta) dbeta[c] += bs;
 }
 
+// workgroups per clip of the dw pass: about four per CU over the batch
+int conv0_dw_blocks(long B, int T0) { return std::min(dfk_cdiv(T0, TB), std::max(1, (int)(1024 / B))); }
+
 }  // namespace
+
+extern "C" int64_t dfk_w2v_conv0_bwd_workspace(int64_t B, int64_t S) {
+  if (B <= 0 || S < KW) return 0;
+  const int T0 = (int)((S - KW) / KS + 1);
+  return (int64_t)4 * (B * CH * 2 + B * conv0_dw_blocks(B, T0) * (int64_t)(CH * KW));
+}
 
 extern "C" int dfk_w2v_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
                                  const float* beta, float eps, float* stats, void* out, int dtype, hipStream_t s) {
@@ -195,19 +228,22 @@ extern "C" int dfk_w2v_conv0_bwd(const float* wave, int64_t B, int64_t S, const 
   if (!wave || !w || !gamma || !beta || !stats || !dout || !scratch || !dw || S < KW) return DFK_EINVAL;
   const int T0 = (int)((S - KW) / KS + 1);
   const dim3 grid(dfk_cdiv(T0, TB), (unsigned)B);
-  const dim3 gdw(std::min(dfk_cdiv(T0, TB), std::max(1, 256 / (int)B)), (unsigned)B);   // ~one workgroup per CU
+  const dim3 gdw(conv0_dw_blocks(B, T0), (unsigned)B);
+  float* part = scratch + B * CH * 2;   // [B * gdw.x][CH * KW] slab after the [B, CH, 2] reductions
   (void)hipMemsetAsync(scratch, 0, sizeof(float) * B * CH * 2, s);
   if (dtype == DFK_BF16) {
     hipLaunchKernelGGL(conv0_bwd_stats<bf16raw>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
                        (const bf16raw*)dout, scratch);
     hipLaunchKernelGGL(conv0_bwd_dw<bf16raw>, gdw, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
-                       (const bf16raw*)dout, scratch, dw);
+                       (const bf16raw*)dout, scratch, part);
   } else {
     hipLaunchKernelGGL(conv0_bwd_stats<float>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
                        (const float*)dout, scratch);
     hipLaunchKernelGGL(conv0_bwd_dw<float>, gdw, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
-                       (const float*)dout, scratch, dw);
+                       (const float*)dout, scratch, part);
   }
+  hipLaunchKernelGGL(dw_slab_sum, dim3(dfk_cdiv(CH * KW, 64), dfk_cdiv(B * gdw.x, 128)), dim3(256), 0, s, part,
+                     (int)(B * gdw.x), dw);
   if (dgamma || dbeta)
     hipLaunchKernelGGL(gn_affine_grad, dim3(dfk_cdiv(CH, 256)), dim3(256), 0, s, scratch, (int)B, dgamma, dbeta);
   DFK_CHECK_LAUNCH();

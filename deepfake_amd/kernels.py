@@ -346,7 +346,8 @@ def w2v_conv0_fwd(wave, w, gamma, beta, eps, dtype):
 
 def w2v_conv0_bwd(wave, w, gamma, beta, eps, stats, dout, dw, dgamma, dbeta):
     B, S = wave.shape
-    scratch = torch.empty(B, 512, 2, device=wave.device, dtype=torch.float32)
+    scratch = torch.empty(max(L.lib().dfk_w2v_conv0_bwd_workspace(B, S) // 4, B * 512 * 2), device=wave.device,
+                          dtype=torch.float32)
     L.check(L.lib().dfk_w2v_conv0_bwd(L.ptr(wave), B, S, L.ptr(w), L.ptr(gamma), L.ptr(beta), float(eps),
                                       L.ptr(stats), L.ptr(dout), L.dt(dout), L.ptr(scratch), L.ptr(dw), L.ptr(dgamma),
                                       L.ptr(dbeta), L.stream()), "w2v_conv0_bwd")

@@ -254,7 +254,9 @@ int dfk_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, hipStr
  * the backward.  The conv output is recomputed, never stored. */
 int dfk_w2v_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
                       const float* beta, float eps, float* stats, void* out, int dtype, hipStream_t stream);
-/* backward: dw [512,10], dgamma, dbeta fp32 (+=); scratch [B,512,2] fp32. */
+/* backward: dw [512,10], dgamma, dbeta fp32 (+=); scratch: dfk_w2v_conv0_bwd_workspace(B, S) bytes of fp32
+ * (the [B,512,2] GroupNorm reductions, then per-workgroup dw partials summed without atomics). */
+int64_t dfk_w2v_conv0_bwd_workspace(int64_t B, int64_t S);
 int dfk_w2v_conv0_bwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
                       const float* beta, float eps, const float* stats, const void* dout, int dtype,
                       float* scratch, float* dw, float* dgamma, float* dbeta, hipStream_t stream);
