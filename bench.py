@@ -35,6 +35,9 @@ import torch.distributed as dist
 # ProcessGroupNCCL watchdog is still polling (with the cache on, the watchdog's query of a
 # capture-recorded event aborts the process: tools/ddp_graph_probe.py).
 os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+# The flight recorder lets the capture observe that the watchdog retired every eager collective
+# (deepfake_amd.ddp.watchdog_idle) instead of guessing with a sleep.
+os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "256")
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -226,8 +229,8 @@ def cpu_baseline(cfg_name, steps):
     """the oracle (CPU restatement of the reference, pinned to the reference's golden
     vectors) timed on the host cores: C1 and C2 at B=2, train-mode BatchNorm, one warm-up step then the
     median of `steps` train steps.  value = the C2 rate (the metric's workload)."""
-    cores = len(os.sched_getaffinity(0))
-    threads = min(cores, 16)
+    cores = len(os.sched_getaffinity(0))   # host CPUs this process may run on
+    threads = min(cores, 16)                # the GPU box's CPU share per GPU is 16
     torch.set_num_threads(threads)
     cpu_model = "unknown"
     try:
@@ -237,10 +240,12 @@ def cpu_baseline(cfg_name, steps):
         pass
     t1 = _cpu_train_rate("c1", 2, steps)
     t2 = _cpu_train_rate(cfg_name, 2, steps)
-    return {"value": round(2.0 / t2, 4), "unit": "clips/s", "cores": threads, "kind": "port",
+    return {"value": round(2.0 / t2, 4), "unit": "clips/s", "cores": threads, "threads": threads,
+            "affinity_cpus": cores, "kind": "port",
             "c1_clips_per_s": round(2.0 / t1, 3), "cpu_model": cpu_model,
             "sample": f"oracle fp32 CPU train step (train-mode BN) at B=2: {cfg_name.upper()} {t2:.2f} s/step, "
-                      f"C1 {t1:.3f} s/step; median of {steps} steps after 1 warm-up, {threads} threads"}
+                      f"C1 {t1:.3f} s/step; median of {steps} steps after 1 warm-up, {threads} torch threads on "
+                      f"{cores} affinity CPUs"}
 
 
 def main():
@@ -315,7 +320,9 @@ def main():
             "config": {"workload": f"{a.config.upper()}: Swin-T video 32x224x224 (window 8x7x7) + SwinV2 mel 224 + "
                                    f"wav2vec2-base 4s@16kHz + FusionModel, full train step",
                        "global_batch": world * a.batch, "per_gpu_batch": a.batch,
-                       "parallelism": f"dp{world}", "hip_graph": not a.eager, "branch_streams": 3,
+                       "parallelism": f"dp{world}", "hip_graph": step.graph is not None,
+                       "captured_overlap": step.captured_overlap, "captured_bn_broadcast": step.captured_bn,
+                       "branch_streams": 3,
                        "regularisers": not a.deterministic, "loss": round(lossv, 5)},
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2) if train_gflop else None,
             "roofline": roof, "roofline_conv3d": roof_conv, "roofline_gemm": roof_gemm, "cpu_baseline": cpu,

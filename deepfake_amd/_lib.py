@@ -103,7 +103,7 @@ SIGNATURES = {
     "dfk_cpb_bias_fwd": [_VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],
     "dfk_cpb_bias_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],
     "dfk_w2v_conv0_fwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP],
-    "dfk_w2v_conv0_bwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _VP, _VP, _VP, _VP],
+    "dfk_w2v_conv0_bwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _I64, _VP, _VP, _VP, _VP],
     "dfk_w2v_conv0_bwd_workspace": [_I64, _I64],
     "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP, _VP],
     "dfk_im2col2d": [_VP, _I64, _VP, C.POINTER(Conv2dGeo), C.c_int, _VP],
@@ -117,6 +117,7 @@ SIGNATURES = {
     "dfk_pool2d_bwd": [_VP, _I64, _VP, _I64, _VP, _I64, C.POINTER(Conv2dGeo), C.c_int, C.c_int, C.c_int, _VP],
     "dfk_dropout": [_VP, _VP, _I64, _I32, _I64, C.POINTER(Drop), C.c_int, _VP],
     "dfk_bernoulli_flags": [C.POINTER(Drop), _I32, _VP, _VP],
+    "dfk_layerdrop_flags": [C.POINTER(Drop), _I32, _VP, _VP, _VP],
     "dfk_spec_augment_fwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _F, _I32, _I32, C.POINTER(Drop), C.c_int, _VP],
     "dfk_spec_augment_bwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, C.c_int, _VP],
     "dfk_frame_normalize": [_VP, _VP, _I64, _I32, _I32, C.POINTER(C.c_float), C.POINTER(C.c_float), _VP],

@@ -38,6 +38,18 @@ __global__ void bernoulli_kernel(const dfk_drop d, int n, float* __restrict__ ou
   out[i] = drop_mul(dc, i, 0) != 0.f ? 1.f : 0.f;
 }
 
+// LayerDrop coins of one micro-step (keep) folded into the accumulation window's "ever kept" flags (used):
+// the SGD gate of a layer is the OR of its coins since the last zero_grad
+__global__ void layerdrop_kernel(const dfk_drop d, int n, float* __restrict__ keep, float* __restrict__ used) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DropCtx dc = drop_ctx(d);
+  dc.mode = 1;
+  const float k = drop_mul(dc, i, 0) != 0.f ? 1.f : 0.f;
+  keep[i] = k;
+  used[i] = fmaxf(used[i], k);
+}
+
 // uniform [0, 1) from a draw
 __device__ __forceinline__ float unit_u(uint32_t h) { return (float)(h >> 8) * (1.f / 16777216.f); }
 
@@ -146,6 +158,14 @@ extern "C" int dfk_bernoulli_flags(const dfk_drop* d, int32_t n, float* out, hip
   if (!out || !drop_args_ok(d)) return DFK_EINVAL;
   if (n <= 0) return 0;
   hipLaunchKernelGGL(bernoulli_kernel, dim3(dfk_cdiv(n, 256)), dim3(256), 0, s, *d, (int)n, out);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_layerdrop_flags(const dfk_drop* d, int32_t n, float* keep, float* used, hipStream_t s) {
+  if (!keep || !used || !drop_args_ok(d)) return DFK_EINVAL;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(layerdrop_kernel, dim3(dfk_cdiv(n, 256)), dim3(256), 0, s, *d, (int)n, keep, used);
   DFK_CHECK_LAUNCH();
   return 0;
 }

@@ -224,8 +224,10 @@ extern "C" int dfk_w2v_conv0_fwd(const float* wave, int64_t B, int64_t S, const 
 
 extern "C" int dfk_w2v_conv0_bwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
                                  const float* beta, float eps, const float* stats, const void* dout, int dtype,
-                                 float* scratch, float* dw, float* dgamma, float* dbeta, hipStream_t s) {
+                                 float* scratch, int64_t scratch_bytes, float* dw, float* dgamma, float* dbeta,
+                                 hipStream_t s) {
   if (!wave || !w || !gamma || !beta || !stats || !dout || !scratch || !dw || S < KW) return DFK_EINVAL;
+  if (scratch_bytes < dfk_w2v_conv0_bwd_workspace(B, S)) return DFK_EINVAL;   // the dw slab is sized per launch
   const int T0 = (int)((S - KW) / KS + 1);
   const dim3 grid(dfk_cdiv(T0, TB), (unsigned)B);
   const dim3 gdw(conv0_dw_blocks(B, T0), (unsigned)B);

@@ -27,10 +27,33 @@ import torch
 import torch.distributed as dist
 
 
+def recorder_on():
+    """The ProcessGroupNCCL flight recorder is on (its size must be set before the process group exists)."""
+    return int(os.environ.get("TORCH_NCCL_TRACE_BUFFER_SIZE", "0") or 0) > 0
+
+
+def watchdog_idle(timeout=60.0):
+    """Wait until the flight recorder lists no collective whose completion the ProcessGroupNCCL watchdog has not
+    yet discovered (onlyActive): then the watchdog queries no event.  Raises on timeout."""
+    import json
+    import time
+    from torch._C import _distributed_c10d as c10d
+    t0 = time.monotonic()
+    while True:
+        d = json.loads(c10d._dump_nccl_trace_json(includeCollectives=True, onlyActive=True))
+        if not d.get("entries"):
+            return
+        if time.monotonic() - t0 > timeout:
+            raise RuntimeError(f"RCCL watchdog still tracks {len(d['entries'])} collectives after {timeout} s")
+        time.sleep(0.002)
+
+
 class GradBucketer:
-    def __init__(self, store, bucket_mb=64.0, group=None):
+    def __init__(self, store, bucket_mb=64.0, group=None, comm_dtype=torch.float32):
         self.store = store
         self.group = group
+        # comm_dtype bf16: each bucket is cast to a bf16 copy right before its all-reduce (half the xGMI bytes:
+        # 425 MB instead of 850 MB per C2 step, SURVEY §7.2) and the sum is cast back, / world, in finish()
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         cap = int(bucket_mb * (1 << 20) / 4)
         self.buckets = []           # (start, end, [param indices])
@@ -61,6 +84,11 @@ class GradBucketer:
         self.bn_buffers = []
         self.streams = []         # branch streams whose kernels write gradients (FusionModel.branch_streams)
         self.comm_stream = None
+        self.comm_dtype = comm_dtype
+        self.cbuf = None
+        if self.enabled and comm_dtype != torch.float32:
+            self.cbuf = torch.zeros(store.grad.numel(), dtype=comm_dtype, device=store.grad.device)
+        self.last_works = []      # the previous eager step's bucket works (drained before a graph capture)
         if self.enabled:
             for i, p in enumerate(store.params):
                 self.hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -93,10 +121,25 @@ class GradBucketer:
     def _make_hook(self, i):
         return lambda _p: self._ready(i)
 
+    def _payload(self, s, e):
+        """The tensor all-reduced for flat range [s, e): the gradient itself, or its bf16 copy."""
+        if self.cbuf is None:
+            return self.store.grad[s:e]
+        c = self.cbuf[s:e]
+        c.copy_(self.store.grad[s:e])
+        return c
+
+    def _unpack(self):
+        """Sum back into the fp32 gradient buffer, averaged over ranks."""
+        if self.cbuf is None:
+            self.store.grad.div_(self.world)
+        else:
+            self.store.grad.copy_(self.cbuf).div_(self.world)
+
     def _launch(self, b):
         s, e, _ = self.buckets[b]
         if not self.streams or not self.store.grad.is_cuda:
-            self.works[b] = dist.all_reduce(self.store.grad[s:e], group=self.group, async_op=True)
+            self.works[b] = dist.all_reduce(self._payload(s, e), group=self.group, async_op=True)
             return
         # a bucket may hold gradients written on several branch streams: issue the all-reduce from a
         # comm stream that waits for all of them (RCCL orders itself after the issuing stream)
@@ -107,7 +150,21 @@ class GradBucketer:
         for st in self.streams:
             cs.wait_stream(st)
         with torch.cuda.stream(cs):
-            self.works[b] = dist.all_reduce(self.store.grad[s:e], group=self.group, async_op=True)
+            self.works[b] = dist.all_reduce(self._payload(s, e), group=self.group, async_op=True)
+
+    def drain(self, works=(), timeout=60.0):
+        """Deterministic drain before a HIP-graph capture.  The ProcessGroupNCCL watchdog thread queries the
+        events of every eager collective until it has seen it complete, and HIP refuses that query once the
+        RCCL stream has joined a capture (the watchdog then aborts the process).  So: wait for the given
+        works, idle the device, then poll the flight recorder (TORCH_NCCL_TRACE_BUFFER_SIZE > 0, set by
+        bench.py / train.py before the process group exists) until the watchdog has retired every eager
+        collective of this process."""
+        for w in works:
+            w.wait()
+        if self.store.grad.is_cuda:
+            torch.cuda.synchronize()
+        if self.enabled and self.store.grad.is_cuda and recorder_on():
+            watchdog_idle(timeout)
 
     def finish(self):
         """After the last micro-step's backward: flush buckets not yet launched (unused
@@ -119,17 +176,19 @@ class GradBucketer:
                 self._launch(b)
         for w in self.works:
             w.wait()
-        self.store.grad.div_(self.world)
+        self.last_works = list(self.works)
+        self._unpack()
         self.reset()
 
     def allreduce_all(self):
         """Non-overlapped variant (used outside a captured graph)."""
         if not self.enabled:
             return
-        works = [dist.all_reduce(self.store.grad[s:e], group=self.group, async_op=True) for s, e, _ in self.buckets]
+        works = [dist.all_reduce(self._payload(s, e), group=self.group, async_op=True) for s, e, _ in self.buckets]
         for w in works:
             w.wait()
-        self.store.grad.div_(self.world)
+        self.last_works = works
+        self._unpack()
 
     def track_batchnorm(self, module):
         """Remember the BatchNorm running statistics that broadcast_bn() refreshes every step."""

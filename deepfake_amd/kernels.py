@@ -349,7 +349,8 @@ def w2v_conv0_bwd(wave, w, gamma, beta, eps, stats, dout, dw, dgamma, dbeta):
     scratch = torch.empty(max(L.lib().dfk_w2v_conv0_bwd_workspace(B, S) // 4, B * 512 * 2), device=wave.device,
                           dtype=torch.float32)
     L.check(L.lib().dfk_w2v_conv0_bwd(L.ptr(wave), B, S, L.ptr(w), L.ptr(gamma), L.ptr(beta), float(eps),
-                                      L.ptr(stats), L.ptr(dout), L.dt(dout), L.ptr(scratch), L.ptr(dw), L.ptr(dgamma),
+                                      L.ptr(stats), L.ptr(dout), L.dt(dout), L.ptr(scratch),
+                                      scratch.numel() * 4, L.ptr(dw), L.ptr(dgamma),
                                       L.ptr(dbeta), L.stream()), "w2v_conv0_bwd")
 
 
@@ -412,6 +413,12 @@ def bernoulli_flags(drop, n, device):
     out = torch.empty(n, device=device, dtype=torch.float32)
     L.check(L.lib().dfk_bernoulli_flags(L.drop(drop, device), n, L.ptr(out), L.stream()), "bernoulli_flags")
     return out
+
+
+def layerdrop_flags(drop, keep, used):
+    """keep[i] = coin i (1 keep / 0 drop), used[i] = max(used[i], keep[i]) — LayerDrop for one micro-step."""
+    L.check(L.lib().dfk_layerdrop_flags(L.drop(drop, keep.device), keep.numel(), L.ptr(keep), L.ptr(used),
+                                        L.stream()), "layerdrop_flags")
 
 
 def spec_augment_fwd(h, embed, mask_prob, mask_length, min_masks, drop):

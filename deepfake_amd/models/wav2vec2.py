@@ -229,13 +229,20 @@ class Wav2Vec2Encoder(nn.Module):
         # dropped layer's parameters stays identical across data-parallel ranks); 1 = run, 0 = skip
         self.layerdrop = rng.Drop(config.layerdrop, shared=True)
         self.register_buffer("layer_keep", torch.ones(config.num_hidden_layers), persistent=False)
+        # OR of the coins since the last zero_grad (the SGD gate): with gradient accumulation a layer kept in
+        # any micro-step of the window has a gradient in the reference (p.grad is not None) and is stepped
+        self.register_buffer("layer_used", torch.zeros(config.num_hidden_layers), persistent=False)
 
     def param_gates(self):
         """(parameters, device flag) pairs for the fused SGD: a layer's parameters are stepped only when its
-        LayerDrop coin kept it (training with layerdrop > 0)."""
+        LayerDrop coin kept it in some micro-step since the last zero_grad (training with layerdrop > 0)."""
         if self.layerdrop.p <= 0:
             return []
-        return [(list(l.parameters()), self.layer_keep[i:i + 1]) for i, l in enumerate(self.layers)]
+        return [(list(l.parameters()), self.layer_used[i:i + 1]) for i, l in enumerate(self.layers)]
+
+    def reset_gates(self):
+        """Called with zero_grad (ParamStore.zero_gates): a new accumulation window starts with no layer kept."""
+        self.layer_used.zero_()
 
     def forward(self, h):
         B, T, C = h.shape
@@ -243,8 +250,7 @@ class Wav2Vec2Encoder(nn.Module):
         x = Fn.layer_norm(self.pos_conv_embed.add_to(h.contiguous()), self.layer_norm, drop=d).reshape(B * T, C)
         lds = self.layerdrop.active(self.training)
         if lds:
-            K.L.check(K.L.lib().dfk_bernoulli_flags(K.L.drop(self.layerdrop.spec(), x.device), len(self.layers),
-                                                    K.L.ptr(self.layer_keep), K.L.stream()), "bernoulli_flags")
+            K.layerdrop_flags(self.layerdrop.spec(), self.layer_keep, self.layer_used)
         for i, layer in enumerate(self.layers):
             y = layer(x, B, T)
             x = torch.where(self.layer_keep[i] > 0, y, x) if lds else y

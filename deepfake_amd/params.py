@@ -90,8 +90,11 @@ class ParamStore:
             p.register_post_accumulate_grad_hook(self._mark(i))
         # device skip flags (LayerDrop): gate[i] is a 1-element fp32 tensor, 0 = leave parameter i untouched
         self.gate = [None] * len(self.params)
+        self.gate_owners = []    # modules whose gates restart with every accumulation window (reset_gates)
         for m in model.modules():
             if hasattr(m, "param_gates"):
+                if hasattr(m, "reset_gates") and m.param_gates():
+                    self.gate_owners.append(m)
                 for ps, flag in m.param_gates():
                     for p in ps:
                         i = self.index.get(id(p))
@@ -138,8 +141,14 @@ class ParamStore:
             K.L.check(K.L.lib().dfk_cast(K.L.ptr(self.flat), K.L.F32, K.L.ptr(self.shadow), K.L.BF16, self.numel,
                                          K.L.stream()), "cast")
 
+    def zero_gates(self):
+        """Device ops only (captured into the step graph with the gradient zeroing)."""
+        for m in self.gate_owners:
+            m.reset_gates()
+
     def zero_grad(self):
         self.grad.zero_()
+        self.zero_gates()
         self.uses.clear()
         self.touched = [False] * len(self.params)
 

@@ -22,7 +22,7 @@ import torch
 import torch.distributed as dist
 
 from . import rng
-from .ddp import GradBucketer
+from .ddp import GradBucketer, recorder_on
 from .optim import CosineAnnealingLR, FusedSGD
 from .params import ParamStore
 from .utils import AverageMeter, Logger
@@ -77,6 +77,8 @@ class TrainStep:
         self.graph_mode = graph
         self.graph = None
         self.static = None
+        self.captured_overlap = None     # form of the captured step (None: not captured)
+        self.captured_bn = False
         self.first_micro = True
         if not bucketer.bn_buffers:
             bucketer.track_batchnorm(model)
@@ -114,43 +116,65 @@ class TrainStep:
             return self.eager(feature, label)
         if self.graph is None:
             return self._capture(feature, label)
-        self.bucketer.broadcast_bn()
+        if not self.captured_bn:
+            self.bucketer.broadcast_bn()
         for s, x in zip(self.static[0], feature):
             s.copy_(x, non_blocking=True)
         self.static[1].copy_(label, non_blocking=True)
         self.graph.replay()
         return self.static[2], self.static[3]
 
+    # capture forms, tried in order (multi-GPU): (bucket all-reduces overlapped with backward, BatchNorm
+    # running-stat broadcast inside the graph)
+    FORMS = ((True, True), (False, True), (False, False))
+
+    def _agree(self, ok):
+        """All ranks commit to a capture form only if every rank captured it (a rank that fell back alone would
+        issue a different collective sequence per step: deadlock or mis-reduction at the first replay)."""
+        if not self.bucketer.enabled:
+            return ok
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.store.flat.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.bucketer.group)
+        return bool(flag.item())
+
     def _capture(self, feature, label):
         """One eager step (initialises momentum, allocator warm-up), then capture the
-        whole step — grad zeroing, fwd, bwd, bucket all-reduces, SGD — as one graph.
+        whole step — grad zeroing, BN broadcast, fwd, bwd, bucket all-reduces, SGD — as one graph.
         Multi-GPU: the bucket all-reduces are captured where the backward completes each bucket (on the
-        comm stream, overlapping the rest of backward, §8e); if the backend cannot capture that form the
-        capture is retried with one all-reduce pass after backward, and only then does the step stay eager."""
+        comm stream, overlapping the rest of backward, §8e); if any rank cannot capture that form, every
+        rank retries with one all-reduce pass after backward, then with the BN broadcast outside the graph,
+        and only then do all ranks run eagerly.
+        RCCL and the capture: the ProcessGroupNCCL watchdog thread queries the events of eager collectives
+        until it retires them, and HIP refuses such a query once the RCCL stream joins a capture (the watchdog
+        then aborts the process).  Every capture attempt therefore starts only after GradBucketer.drain has
+        observed, through the flight recorder, that the watchdog retired every eager collective; the
+        capture runs in thread-local mode so no other thread's legal call can invalidate it."""
         loss, prob = self.eager(feature, label)
-        torch.cuda.synchronize()
-        if self.bucketer.enabled:
-            # let the ProcessGroupNCCL watchdog retire the eager step's RCCL works before the capture: it polls
-            # their events, and HIP refuses an event query while that event's stream (the RCCL stream, which
-            # the captured all-reduces join) is capturing — the watchdog thread then aborts the process
-            time.sleep(1.0)
         static_in = [x.clone() for x in feature]
         static_label = label.clone()
         err = None
-        forms = (True, False) if self.bucketer.enabled else (False,)
-        if os.environ.get("DFK_CAPTURE_OVERLAP") == "0":   # probes: only the one-pass form
-            forms = (False,)
-        for overlap in forms:
+        forms = self.FORMS if self.bucketer.enabled else ((False, False),)
+        if os.environ.get("DFK_CAPTURE_OVERLAP") == "0":   # probes: only the one-pass forms
+            forms = tuple(f for f in forms if not f[0])
+        if self.bucketer.enabled and not recorder_on():   # the same environment on every rank: all go eager
+            forms = ()
+            err = RuntimeError("TORCH_NCCL_TRACE_BUFFER_SIZE unset: the RCCL watchdog cannot be observed idle")
+        for overlap, bn in forms:
+            self.bucketer.drain(self.bucketer.last_works)
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             self.bucketer.overlap = overlap
             self.bucketer.reset()
             self.store.uses.clear()   # a failed attempt may have left forward-use counts behind
+            ok = True
             try:
                 with torch.cuda.stream(s):
-                    with torch.cuda.graph(g, stream=s):
+                    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                         self.store.grad.zero_()
+                        self.store.zero_gates()
+                        if bn:
+                            self.bucketer.broadcast_bn()
                         l2, p2 = self._fwd_bwd(tuple(static_in), static_label)
                         if overlap:
                             self.bucketer.finish()         # flush unused buckets, join the comm stream, average
@@ -159,14 +183,17 @@ class TrainStep:
                         self.opt.step(first=False)
             except RuntimeError as e:         # e.g. a collective the backend cannot capture in this form
                 torch.cuda.synchronize()
-                err = e
-                continue
+                err, ok = e, False
             torch.cuda.current_stream().wait_stream(s)
+            if not self._agree(ok):
+                del g
+                continue
             self.bucketer.overlap = True
             self.bucketer.reset()
             self.graph = g
             self.static = (static_in, static_label, l2, p2)
             self.captured_overlap = overlap
+            self.captured_bn = bn
             return loss, prob
         self.bucketer.overlap = True
         self.bucketer.reset()
@@ -193,6 +220,10 @@ class Trainer:
         self.trainloader = dataset.train_dataloader()
         self.valloader = dataset.val_dataloader()
         dt = compute_dtype or (torch.bfloat16 if getattr(args, "dtype", "bf16") == "bf16" else torch.float32)
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        # device-side regulariser streams from --random_seed: per-rank element masks (dropout, DropPath,
+        # SpecAugment), one shared stream for the LayerDrop coins (train.py:67 seed_torch seeds only torch)
+        rng.manual_seed(int(getattr(args, "random_seed", 0)), self.rank)
         model.to(device)
         self.model_s = self.model = model
         self.store = ParamStore(model, dt)
@@ -206,7 +237,6 @@ class Trainer:
         self.scheduler = CosineAnnealingLR(self.optimizer, T_max=self.train_epochs * steps_per_epoch)
         self.step_fn = TrainStep(model, self.store, self.optimizer, self.bucketer, graph=graph)
         self.lossF = torch.nn.BCELoss()
-        self.rank = dist.get_rank() if dist.is_initialized() else 0
         n = sum(p.numel() for p in model.parameters())
         self.logger(f"model params: {n / 1e6:.3f} M ({n * 4 / 2 ** 20:.1f} MiB fp32)")
 

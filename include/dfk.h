@@ -254,12 +254,14 @@ int dfk_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, hipStr
  * the backward.  The conv output is recomputed, never stored. */
 int dfk_w2v_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
                       const float* beta, float eps, float* stats, void* out, int dtype, hipStream_t stream);
-/* backward: dw [512,10], dgamma, dbeta fp32 (+=); scratch: dfk_w2v_conv0_bwd_workspace(B, S) bytes of fp32
- * (the [B,512,2] GroupNorm reductions, then per-workgroup dw partials summed without atomics). */
+/* backward: dw [512,10], dgamma, dbeta fp32 (+=); scratch: fp32 buffer of scratch_bytes >=
+ * dfk_w2v_conv0_bwd_workspace(B, S) bytes (the [B,512,2] GroupNorm reductions, then per-workgroup dw partials
+ * summed without atomics); a smaller buffer returns DFK_EINVAL. */
 int64_t dfk_w2v_conv0_bwd_workspace(int64_t B, int64_t S);
 int dfk_w2v_conv0_bwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
                       const float* beta, float eps, const float* stats, const void* dout, int dtype,
-                      float* scratch, float* dw, float* dgamma, float* dbeta, hipStream_t stream);
+                      float* scratch, int64_t scratch_bytes, float* dw, float* dgamma, float* dbeta,
+                      hipStream_t stream);
 
 /* SwinV2 cosine-attention prologue (swin_transformer2d.py:154-157) on a [rows, 3C]
  * qkv buffer: q' = normalize(q)*scale[h], k' = normalize(k), v' = v, so the window
@@ -303,6 +305,11 @@ int dfk_dropout(const void* x, void* y, int64_t rows, int32_t cols, int64_t ld, 
 /* out[i] = keep(draw i) ? 1 : 0 for i < n (fp32): the per-layer LayerDrop coins of the wav2vec2 encoder
  * (HF :700-706: skip layer when rand < layerdrop), drawn on the device so a replayed graph re-draws them. */
 int dfk_bernoulli_flags(const dfk_drop* drop, int32_t n, float* out, hipStream_t stream);
+/* The same coins for one micro-step of an accumulation window: keep[i] = coin i, and used[i] = max(used[i],
+ * keep[i]) — the SGD gate of layer i is the OR of its coins over the window (the caller zeroes `used` with the
+ * gradients): torch's SGD steps a parameter whose accumulated .grad is not None, i.e. whose layer ran in ANY
+ * micro-step of the window (src/trainer.py:280-297 with HF :700-706). */
+int dfk_layerdrop_flags(const dfk_drop* drop, int32_t n, float* keep, float* used, hipStream_t stream);
 /* SpecAugment time masking (HF Wav2Vec2Model._mask_hidden_states :1272-1317 with _compute_mask_indices
  * :101-218, no attention mask): per clip, num = max(min_masks, int(mask_prob*T/mask_length + eps)) (eps one
  * uniform draw per call, num clamped as HF does) distinct span starts drawn uniformly from [0, T-mask_length],

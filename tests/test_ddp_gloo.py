@@ -75,7 +75,7 @@ def _worker(rank, world, port, overlap, q):
     if rank == 0:
         m.bn.running_mean.fill_(3.0)
     bk.broadcast_buffers(m)
-    q.put((rank, store.grad.clone(), m.bn.running_mean.clone()))
+    q.put((rank, store.grad.numpy().copy(), m.bn.running_mean.numpy().copy()))   # by value: the worker exits
     dist.destroy_process_group()
 
 
@@ -123,7 +123,7 @@ def _accum_worker(rank, world, port, q):
         if k < ACC - 1:
             launched_early.append(any(w is not None for w in bk.works))
     step.bucketer.broadcast_bn()
-    q.put((rank, store.flat.clone(), m.bn.running_mean.clone(), launched_early))
+    q.put((rank, store.flat.numpy().copy(), m.bn.running_mean.numpy().copy(), launched_early))
     dist.destroy_process_group()
 
 
@@ -135,7 +135,7 @@ def test_accumulation_no_sync_matches_single_process_sum():
     procs = [ctx.Process(target=_accum_worker, args=(r, 2, 29513, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (f, rm, le)) for r, f, rm, le in (q.get(timeout=120) for _ in procs))
+    res = dict((r, (torch.from_numpy(f), torch.from_numpy(rm), le)) for r, f, rm, le in (q.get(timeout=120) for _ in procs))
     for p in procs:
         p.join(timeout=60)
     torch.manual_seed(0)
@@ -163,7 +163,7 @@ def test_bucketed_allreduce_matches_global_batch(overlap):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, overlap, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (g, rm)) for r, g, rm in (q.get(timeout=120) for _ in procs))
+    res = dict((r, (torch.from_numpy(g), torch.from_numpy(rm))) for r, g, rm in (q.get(timeout=120) for _ in procs))
     for p in procs:
         p.join(timeout=60)
     # reference: per-shard BN statistics, gradient averaged over the 2 shards (= DDP semantics)
@@ -178,3 +178,105 @@ def test_bucketed_allreduce_matches_global_batch(overlap):
     for r in range(2):
         assert torch.allclose(res[r][0], ref, atol=1e-6), (r, (res[r][0] - ref).abs().max())
         assert torch.all(res[r][1] == 3.0)
+
+
+def _layout_worker(rank, world, port, comm, q):
+    """The real fused C1 model's parameter list in the ParamStore (reverse registration order, adjacency groups,
+    16-B aligned gaps, 4 MB buckets): CPU stand-in gradients reported ready in backward order through the
+    direct-gradient protocol (ParamStore.grad_ready), as the HIP backward kernels report them."""
+    from deepfake_amd.models.fused import build_fused
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = build_fused("c1")
+    store = ParamStore(m, torch.float32, device=torch.device("cpu"))
+    bk = GradBucketer(store, bucket_mb=4.0, comm_dtype=comm)
+    launched = []
+    for i in range(len(store.params)):
+        p = store.params[i]
+        g = torch.Generator().manual_seed(1000 * rank + i)
+        p.grad.copy_(torch.randn(p.shape, generator=g))
+        store.grad_ready(p)
+        launched.append(sum(w is not None for w in bk.works))
+    bk.finish()
+    q.put((rank, store.grad.numpy().copy(), launched, len(bk.buckets)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("comm", ["fp32", "bf16"])
+def test_fused_model_bucket_layout(comm):
+    """world 2: the bucketed all-reduce over the real fused C1 parameter layout (341 tensors, 49.4 M values)
+    gives the mean of the ranks' gradients; buckets launch during the backward, not all at the end.
+    bf16 buckets (half the xGMI bytes): within 8e-3 of the fp32 mean relative to each element's scale
+    (one bf16 rounding per rank's value and one per partial sum)."""
+    from deepfake_amd.models.fused import build_fused
+    dt = torch.bfloat16 if comm == "bf16" else torch.float32
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29521 if comm == "fp32" else 29523
+    procs = [ctx.Process(target=_layout_worker, args=(r, 2, port, dt, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (torch.from_numpy(g), la, nb)) for r, g, la, nb in (q.get(timeout=240) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+    m = build_fused("c1")
+    store = ParamStore(m, torch.float32, device=torch.device("cpu"))
+    ref = torch.zeros_like(store.grad)
+    scale = torch.zeros_like(store.grad)
+    for rank in range(2):
+        for i, p in enumerate(store.params):
+            g = torch.Generator().manual_seed(1000 * rank + i)
+            s, e = store.span(i)
+            v = torch.randn(p.shape, generator=g).reshape(-1)
+            ref[s:e] += v / 2
+            scale[s:e] += v.abs() / 2
+    for r in range(2):
+        got, launched, nb = res[r]
+        assert nb > 4 and launched[len(launched) // 2] > 0, "buckets must launch during the backward"
+        if comm == "fp32":
+            assert torch.allclose(got, ref, atol=1e-6, rtol=0)
+        else:
+            assert bool(((got - ref).abs() <= 8e-3 * scale + 1e-6).all()), float((got - ref).abs().max())
+    assert torch.equal(res[0][0], res[1][0])
+
+
+class _Args:
+    epochs, learning_rate, batch_size, modality, model_save, log_step = 1, 0.1, 2, "fused", 0, 1
+    accum_step, l2_decacy, random_seed, bucket_mb = 1, 0.0, 42, 1.0
+
+
+class _Data:
+    def train_dataloader(self):
+        return []
+
+    def val_dataloader(self):
+        return None
+
+
+def _seed_worker(rank, world, port, q):
+    from deepfake_amd import rng
+    from deepfake_amd.trainer import Trainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    Trainer(Net(), _Args(), torch.device("cpu"), _Data(), compute_dtype=torch.float32)
+    q.put((rank, rng.state("cpu").tolist()))
+    dist.destroy_process_group()
+
+
+def test_trainer_seeds_device_rng_per_rank():
+    """Trainer seeds the device regulariser streams from --random_seed and the rank: element masks differ
+    per rank (independent clip shards), the LayerDrop stream is shared (identical skips on every replica)."""
+    from deepfake_amd import rng
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_seed_worker, args=(r, 2, 29525, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    st = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert st[0][0] != st[1][0]
+    assert st[0][2] == st[1][2]
+    rng.manual_seed(42, 1)
+    assert rng.state("cpu").tolist()[0] == st[1][0]

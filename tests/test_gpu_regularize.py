@@ -239,3 +239,48 @@ def test_fused_c1_regularized_step():
         assert torch.isfinite(store.flat).all()
     assert all(math.isfinite(v) for v in losses)
     assert len(set(losses)) == 3
+
+
+def test_layerdrop_gate_is_or_over_accumulation_window():
+    """Gradient accumulation with LayerDrop (reference defaults: --accum_step 4, layerdrop 0.1): torch's SGD
+    steps a layer's parameters iff their accumulated .grad is not None, i.e. iff the layer ran in ANY micro-step
+    of the window (src/trainer.py:280-297, HF :700-706).  The fused SGD's gate must be the OR of the coins, not
+    the last micro-step's coin: a layer kept earlier but dropped last is still stepped with the accumulated
+    gradient; a layer dropped in every micro-step is left untouched (parameters and momentum)."""
+    from deepfake_amd.models import set_compute_dtype
+    from deepfake_amd.models.fused import W2V_CONFIG
+    from deepfake_amd.models.wav2vec2 import Wav2Vec2Config, Wav2Vec2Encoder
+    from deepfake_amd.optim import FusedSGD
+    from deepfake_amd.params import ParamStore
+    torch.manual_seed(0)
+    rng.manual_seed(11, 0)
+    cfg = Wav2Vec2Config.from_json_file(W2V_CONFIG, num_hidden_layers=8).deterministic()
+    cfg.layerdrop = 0.5
+    enc = set_compute_dtype(Wav2Vec2Encoder(cfg), torch.float32).to(DEV).train()
+    store = ParamStore(enc, torch.float32)
+    store.zero_grad()
+    opt = FusedSGD(store, 0.1, 0.9, 0.05)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    h = torch.randn(2, 49, 768, device=DEV, generator=g)
+    wy = torch.randn(2, 49, 768, device=DEV, generator=g)
+    coins = []
+    for _ in range(4):
+        rng.advance(DEV)
+        (enc(h).float() * wy).sum().backward()
+        coins.append(enc.layer_keep.clone())
+    c = torch.stack(coins)
+    used = c.amax(0)
+    assert torch.equal(enc.layer_used, used)
+    assert bool(((c[-1] == 0) & (used == 1)).any()), "seed must exercise kept-then-dropped"
+    p0, g0 = store.flat.clone(), store.grad.clone()
+    opt.step()
+    for i, layer in enumerate(enc.layers):
+        for p in layer.parameters():
+            s, e = store.span(store.index[id(p)])
+            if used[i] == 0:
+                assert torch.equal(store.flat[s:e], p0[s:e]) and torch.equal(opt.buf[s:e], torch.zeros_like(opt.buf[s:e]))
+            else:
+                want = p0[s:e] - 0.1 * (g0[s:e] + 0.05 * p0[s:e])
+                assert rel(store.flat[s:e], want) < 1e-6, (i, rel(store.flat[s:e], want))
+    store.zero_grad()
+    assert torch.equal(enc.layer_used, torch.zeros_like(enc.layer_used))

@@ -59,12 +59,15 @@ def test_graph_captured_step_matches_eager():
 def test_captured_overlapped_allreduce_single_rank():
     """The step graph with the bucket all-reduces captured where backward completes each bucket (§8e):
     one RCCL rank on the box's GPU (DFK_DDP_FORCE=1 enables the bucketer at world size 1), C1, eager vs
-    graph-replayed steps — the overlapped form must be the one captured and the parameters must agree."""
+    graph-replayed steps — the overlapped form (BatchNorm broadcast inside the graph) must be the one captured
+    and the parameters must agree.  No sleep: the capture waits until the flight recorder shows the watchdog
+    retired the eager replica's fresh RCCL works (deepfake_amd.ddp.watchdog_idle)."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, DFK_DDP_FORCE="1", TORCH_NCCL_CUDA_EVENT_CACHE="0", MASTER_ADDR="127.0.0.1")
+    env = dict(os.environ, DFK_DDP_FORCE="1", TORCH_NCCL_CUDA_EVENT_CACHE="0", TORCH_NCCL_TRACE_BUFFER_SIZE="256",
+               MASTER_ADDR="127.0.0.1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
                         "--master-addr", "127.0.0.1", "--master-port", "29531",
                         os.path.join(root, "tools", "ddp_graph_probe.py"), "c1"],
@@ -72,4 +75,5 @@ def test_captured_overlapped_allreduce_single_rank():
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert "captured overlapped all-reduces: True" in out, out[-3000:]
+    assert "captured BN broadcast: True" in out, out[-3000:]
     assert "\nok" in out, out[-3000:]

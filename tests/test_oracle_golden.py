@@ -1,6 +1,5 @@
 """Pin the CPU oracle to the reference's own outputs (golden fixtures generated
 by importing /root/reference, tests/golden/make_golden.py).  CPU only."""
-import types
 
 import pytest
 import torch
@@ -164,6 +163,3 @@ def test_swinv2_masks_match_reference_construction():
     m = S2.shift_mask_2d(14, 14, 7, 3)
     assert m.shape == (4, 49, 49) and set(m.unique().tolist()) == {0.0, -100.0}
 
-
-def test_config_types():
-    assert isinstance(types.SimpleNamespace(), object)

@@ -10,6 +10,9 @@ import time
 import torch
 import torch.distributed as dist
 
+os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "256")
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import synthetic_batch  # noqa: E402
 from deepfake_amd import rng  # noqa: E402
@@ -39,14 +42,13 @@ def make(graph):
 
 feat, label = synthetic_batch(cfg, B, torch.device("cuda"), 3)
 ge, se = make(False)
-le = [ge(feat, label)[0].item() for _ in range(3)]   # the eager replica first: no RCCL work of another
-torch.cuda.synchronize()                              # TrainStep may be in flight while the graph is captured
-time.sleep(1.0)
-gg, sg = make(True)
+le = [ge(feat, label)[0].item() for _ in range(3)]   # the eager replica's RCCL works are fresh when the
+gg, sg = make(True)                                   # graph replica captures: TrainStep drains the watchdog
 lg = [gg(feat, label)[0].item() for _ in range(3)]
 for i in range(3):
     print(f"step {i}: eager loss {le[i]:.6f}  graph loss {lg[i]:.6f}", flush=True)
 print("captured overlapped all-reduces:", getattr(gg, "captured_overlap", None))
+print("captured BN broadcast:", getattr(gg, "captured_bn", None))
 d = (se.flat - sg.flat).abs().max().item() / se.flat.abs().max().item()
 print(f"max |param diff| / max |param| after 3 steps: {d:.3e}")
 assert d < 1e-2, d
