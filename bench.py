@@ -37,7 +37,7 @@ import torch.distributed as dist
 os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 # The flight recorder lets the capture observe that the watchdog retired every eager collective
 # (deepfake_amd.ddp.watchdog_idle) instead of guessing with a sleep.
-os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "256")
+os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "256")
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
@@ -86,8 +86,8 @@ def time_kernel(fn, iters):
     return s.elapsed_time(e) / iters * 1e-3   # seconds per launch
 
 
-ROOFLINE_KERNEL = "wattn_fwd_tab_kernel<32>"
-ROOFLINE_PMC = os.path.join(HERE, "profiles", "r2_wattn_fwd_pmc.json")
+ROOFLINE_KERNEL = "wattn_fwd3_kernel<32, true, false>"
+ROOFLINE_PMC = os.path.join(HERE, "profiles", "r3_wattn_fwd_pmc.json")
 
 
 def roofline_case(cfg, B, dt):
@@ -108,8 +108,8 @@ def roofline_case(cfg, B, dt):
     rpb = torch.randn(15 * 13 * 13, heads, device="cuda", generator=g) * 0.02
     out = torch.empty(rows, C, device="cuda", dtype=dt)
     args = (qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, (B, D, H, W), win, win, (4, 3, 3), heads, hd, hd ** -0.5)
-    # the score-bias table (dfk_wattn_table, a separate launch) is built once: the timed launch is the
-    # attention kernel alone, the one rocprofv3 lists as wattn_fwd_tab_kernel<32>
+    # the bf16 score-bias tiles (dfk_wattn_table, a separate launch) are built once: the timed launch is the
+    # attention kernel alone, the one rocprofv3 lists as wattn_fwd3_kernel<32, true, false>
     _, _, tab = K.wattn_fwd(*args, rpb=rpb, out=out, return_table=True)
 
     def run():

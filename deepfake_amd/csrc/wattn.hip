@@ -562,53 +562,6 @@ __device__ __forceinline__ int tab_token(const dfk_wattn_args& a, int i) {
   return pos << 3 | bits;
 }
 
-// Block (chunk, class*heads + head): token records and the head's RPB column (/ scale) in LDS, then
-// one thread per 16-B lane slot of the fwd layout (8 values) or 32-B slot of the bwd layout (16).
-__global__ __launch_bounds__(256) void wattn_tab_kernel(const dfk_wattn_args a, const Geo g, long nf, long nb,
-                                                        float* __restrict__ tf, float* __restrict__ tb) {
-  extern __shared__ int tsm[];
-  int* tok = tsm;                                          // [Np]
-  float* rp = reinterpret_cast<float*>(tsm + g.Np);        // [L]
-  const int ch = blockIdx.y, h = ch % a.heads, cls = ch / a.heads;
-  const float inv_scale = 1.f / a.scale, pen = -100.f * inv_scale;
-  for (int i = threadIdx.x; i < g.Np; i += blockDim.x) tok[i] = i < g.N ? tab_token(a, i) : 0;
-  for (int l = threadIdx.x; l < g.L; l += blockDim.x) rp[l] = a.rpb ? a.rpb[(long)l * a.heads + h] * inv_scale : 0.f;
-  __syncthreads();
-  auto val = [&](int q, int k) -> float {
-    if (k >= g.N) return -INFINITY;
-    if (q >= g.N) return 0.f;
-    const int tq = tok[q], tk = tok[k];
-    float v = rp[(tq >> 3) - (tk >> 3) + g.C0];
-    if ((tq ^ tk) & cls & 7) v += pen;
-    return v;
-  };
-  const int nq16 = g.Np / 16, nk32 = g.Np / 32;
-  const long per_f = (long)nq16 * nk32 * 64, per_b = (long)nk32 * nk32 * 64;   // slots per (class, head)
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < per_f + (nb ? per_b : 0);
-       t += (long)gridDim.x * blockDim.x) {
-    const int lane = (int)(t & 63), grp = lane >> 4, ql = lane & 15;
-    if (t < per_f) {
-      const long u = t >> 6;
-      const int kb = (int)(u % nk32), qt = (int)(u / nk32);
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = val(qt * 16 + ql, kb * 32 + (j >> 2) * 16 + grp * 4 + (j & 3));
-      float* dst = tf + (ch * per_f + t) * 8;
-      *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
-    } else {
-      const long tt = t - per_f, u = tt >> 6;
-      const int kb = (int)(u % nk32), qb = (int)(u / nk32);
-      float v[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = val(qb * 32 + (j >> 3) * 16 + grp * 4 + (j & 3), kb * 32 + ((j >> 2) & 1) * 16 + ql);
-      float* dst = tb + (ch * per_b + tt) * 16;
-#pragma unroll
-      for (int j = 0; j < 16; j += 4) *reinterpret_cast<float4*>(dst + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
-    }
-  }
-}
-
 TabGeo tab_geo(const dfk_wattn_args& a, const Geo& g) {
   TabGeo t;
   t.ncls = g.use_mask ? 8 : 1;
@@ -621,6 +574,10 @@ long tab_elems(const dfk_wattn_args& a, const Geo& g) {
   const TabGeo t = tab_geo(a, g);
   return (long)t.ncls * a.heads * t.per_ch;
 }
+
+// bf16 tables, fwd layout then bwd layout
+long tab3_bytes(const dfk_wattn_args& a, const Geo& g) { return 2L * 2 * tab_elems(a, g); }
+bf16raw* tab3_fwd(const dfk_wattn_args& a, const Geo& g) { return reinterpret_cast<bf16raw*>(a.tab); }
 
 // the window's shift class (table index): one bit per shifted dim, set for the last window along it
 __device__ __forceinline__ int win_class(const dfk_wattn_args& a, const Geo& g, int win) {
@@ -680,25 +637,111 @@ __device__ __forceinline__ float grp_max4(float v) {
   return fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
 }
 
-// Forward with the bias table.  Work order: decode_unit (class/head-sorted, XCD-chunked).  One
-// workgroup = one (clip, window, head): K/V staged once into swizzled LDS tiles (the only LDS: three
-// workgroups fit a CU at 392-token windows); per wave 32 queries against 32-key blocks: S^T = K Q^T +
-// table (the fp32 table tile is loaded straight into the accumulators, two key blocks ahead), running
-// max in raw units, P = 2^(S*scale*log2e - m) by one fma + exp per score, lazy rescale,
-// O^T += V^T P^T, l = ones^T P^T (the denominator on the MFMA too).
-template <int HD, bool DROP = false>
-__global__ __launch_bounds__(256) void wattn_fwd_tab_kernel(const dfk_wattn_args a, const Geo g, int qsplit,
-                                                            const float* __restrict__ tab) {
+// ------------------------------------------------- v3: bf16 bias tiles + 32x32x16 MFMA (forward)
+// Score bias in log2 units, bf16, in the operand order of the MFMA that adds it:
+//   bias'(q, k) = (rpb[pos(q) - pos(k) + C0] + (label(q) != label(k) ? -100 : 0)) * log2(e),
+//   -1e4 for keys >= N (finite: the identity product below must never meet an infinity), 0 for queries >= N.
+// A 32x32 score tile gets its bias from two v_mfma_f32_32x32x16_bf16 products bias_c x I_c (c = query half):
+// I_c[slot][n] = (slot == n - 16c) is a constant identity operand, so the add costs two MFMA issues and
+// no VALU, and the tile streams as 2 KB of bf16 instead of 4 KB of fp32.
+//   fwd layout (S^T: key on the row, query on the lane) [cls][head][qb][kb][c][64 lanes][8]:
+//       lane l, element j <-> k = 32 kb + (l & 31), q = 32 qb + 16 c + 8 (l >> 5) + j
+//   bwd layout (S: query on the row, key on the lane)  [cls][head][qb][kb][c][64 lanes][8]:
+//       lane l, element j <-> q = 32 qb + (l & 31), k = 32 kb + 16 c + 8 (l >> 5) + j
+constexpr float kPadKey = -1.0e4f;
+
+__global__ __launch_bounds__(256) void wattn_tab3_kernel(const dfk_wattn_args a, const Geo g, bf16raw* __restrict__ tf,
+                                                         bf16raw* __restrict__ tb) {
+  extern __shared__ int tsm[];
+  int* tok = tsm;                                          // [Np]
+  float* rp = reinterpret_cast<float*>(tsm + g.Np);        // [L]
+  const int ch = blockIdx.y, h = ch % a.heads, cls = ch / a.heads;
+  const float pen = -100.f * kLog2e;
+  for (int i = threadIdx.x; i < g.Np; i += blockDim.x) tok[i] = i < g.N ? tab_token(a, i) : 0;
+  for (int l = threadIdx.x; l < g.L; l += blockDim.x) rp[l] = a.rpb ? a.rpb[(long)l * a.heads + h] * kLog2e : 0.f;
+  __syncthreads();
+  auto val = [&](int q, int k) -> float {
+    if (k >= g.N) return kPadKey;
+    if (q >= g.N) return 0.f;
+    const int tq = tok[q], tk = tok[k];
+    float v = rp[(tq >> 3) - (tk >> 3) + g.C0];
+    if ((tq ^ tk) & cls & 7) v += pen;
+    return v;
+  };
+  const int nkb = g.Np / 32;
+  const long slots = (long)g.Np * g.Np / 8;   // 16-B slots per layout per (class, head)
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < 2 * slots; t += (long)gridDim.x * blockDim.x) {
+    const bool bwd = t >= slots;
+    const long u = bwd ? t - slots : t;
+    const int lane = (int)(u & 63), c = (int)((u >> 6) & 1);
+    const long blk = u >> 7;
+    const int kb = (int)(blk % nkb), qb = (int)(blk / nkb);
+    const int rr = lane & 31, hh = lane >> 5;
+    uint4 w;
+    uint32_t* pw = reinterpret_cast<uint32_t*>(&w);
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      float v0, v1;
+      if (!bwd) {
+        v0 = val(qb * 32 + 16 * c + 8 * hh + j, kb * 32 + rr);
+        v1 = val(qb * 32 + 16 * c + 8 * hh + j + 1, kb * 32 + rr);
+      } else {
+        v0 = val(qb * 32 + rr, kb * 32 + 16 * c + 8 * hh + j);
+        v1 = val(qb * 32 + rr, kb * 32 + 16 * c + 8 * hh + j + 1);
+      }
+      pw[j >> 1] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
+    }
+    *reinterpret_cast<uint4*>((bwd ? tb : tf) + ((long)ch * slots + u) * 8) = w;
+  }
+}
+
+// identity operands of the bias product (B[slot][n] = slot == n - 16c), and the row-sum selector: a
+// v_mfma_f32_16x16x32_bf16 A operand (lane l: row l & 15, k = 8 (l >> 4) + j) that is 1 iff row == (l >> 4) & 1,
+// so that with a 32x32x16 B fragment X (query l & 31 on the lane) the 16x16 product's row 0 / row 1 hold the
+// column sums of X for queries 0-15 / 16-31 — in lanes 0-15, registers 0 / 1 (4 accumulator registers, not 16)
+__device__ __forceinline__ void bias_ident(int lane, bf16x8& i0, bf16x8& i1, bf16x8& sel) {
+  const int r = lane & 31, hh = lane >> 5;
+  const float sv = (lane & 15) == ((lane >> 4) & 1) ? 1.f : 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    i0[j] = (__bf16)(8 * hh + j == r ? 1.f : 0.f);
+    i1[j] = (__bf16)(8 * hh + j + 16 == r ? 1.f : 0.f);
+    sel[j] = (__bf16)sv;
+  }
+}
+
+// the row sum of query r (= lane & 31) from the selector accumulator: lane r & 15, register r >> 4
+__device__ __forceinline__ float selsum(const f32x4& l4, int lane) {
+  const int r = lane & 31;
+  const float v0 = __shfl(l4[0], r & 15, 64), v1 = __shfl(l4[1], r & 15, 64);
+  return r < 16 ? v0 : v1;
+}
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Forward v3.  One workgroup = one (clip, window, head) (x qsplit), 4 waves; K and V of the window staged once
+// in XOR-swizzled LDS tiles.  Per wave and 32-query block, per 32-key block:
+//   D = K Q'^T + bias' - m        (Q' = Q * scale * log2e; -m enters as the C input of the first MFMA: a
+//                                  16-register tile held per lane, rewritten only on a rescale)
+//   P = 2^D                        (one v_exp per score, no subtract, no multiply)
+//   O^T += V^T P^T, l = ones^T P^T (both on the MFMA; P^T is the accumulator tile converted in place)
+// with a lazy rescale (m moves only when a block's max exceeds it by kRescale, or on the first block).
+// Lane l holds query 32 qb + (l & 31) and keys (j & 3) + 8 (j >> 2) + 4 (l >> 5) of every tile.
+template <int HD, bool TAB, bool DROP>
+__global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_kernel(const dfk_wattn_args a, const Geo g, int qsplit,
+                                                         const bf16raw* __restrict__ tab) {
+  constexpr int NKK = HD / 16, NOT = HD / 32, CH = HD / 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16raw* Ks = reinterpret_cast<bf16raw*>(smem);
   bf16raw* Vs = Ks + (size_t)g.Np * HD;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int grp = lane >> 4, ql = lane & 15, tq = ql >> 2, tp = ql & 3;
+  const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const WUnit wu = decode_unit(a, g, qsplit);
   const int head = wu.head, win = wu.win, b = wu.b;
   const long unit = wu.lse_unit;
   const int hoff = head * HD;
-  constexpr int CH = HD / 8;
   for (int idx = tid; idx < g.Np * CH; idx += blockDim.x) {
     const int i = idx / CH, c = (idx % CH) * 8;
     const int row = token_info_row(a, g, b, win, i);
@@ -706,175 +749,140 @@ __global__ __launch_bounds__(256) void wattn_fwd_tab_kernel(const dfk_wattn_args
     *reinterpret_cast<uint4*>(Vs + swz<HD>(i, c)) = tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + c);
   }
   const int nkb = g.Np / 32, nqb = g.Np / 32;
-  const float* tch = tab + ((long)wu.cls * a.heads + head) * (long)g.Np * g.Np;
+  const bf16raw* tch = TAB ? tab + ((long)wu.cls * a.heads + head) * (long)g.Np * g.Np : nullptr;
+  bf16x8 id0, id1, sel;
+  bias_ident(lane, id0, id1, sel);
+  const float qs = a.scale * kLog2e;
+  const DropCtx dc = drop_ctx(a.drop);
   __syncthreads();
 
-  const float scale2 = a.scale * kLog2e;
-  const DropCtx dc = drop_ctx(a.drop);   // DROP: attention-probability dropout (row = unit*Np + q, col = k)
-  bf16x8 ones;
+  const int nw = blockDim.x >> 6, qstep = nw * qsplit;
+  int qrown;
+  bf16x8 qfn[NKK];
+  auto load_q = [&](int qb) {   // Q'^T B operands of query 32 qb + r: elements 8 hh + j of each 16-wide k-step
+    const int q = qb * 32 + r;
+    qrown = q < g.N ? token_info_row(a, g, b, win, q) : -2;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
-  const int nw = blockDim.x >> 6;
-  // Q fragments of the wave's next query block are loaded one block ahead (their latency hides under
-  // the current block's key sweep)
-  int qrown[2];
-  bf16x8 qfn[2][HD / 32];
-  auto load_q = [&](int qb) {
-#pragma unroll
-    for (int qh = 0; qh < 2; ++qh) {
-      const int q = qb * 32 + qh * 16 + ql;
-      qrown[qh] = q < g.N ? token_info_row(a, g, b, win, q) : -2;
-#pragma unroll
-      for (int es = 0; es < HD / 32; ++es)
-        qfn[qh][es] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.q, a.pad_q, qrown[qh], a.ld_qkv, hoff + es * 32 + grp * 8));
-    }
+    for (int kk = 0; kk < NKK; ++kk)
+      qfn[kk] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.q, a.pad_q, qrown, a.ld_qkv, hoff + kk * 16 + hh * 8));
   };
-  const int qstep = nw * qsplit;
   load_q(min(wu.qpart * nw + wave, nqb - 1));
   for (int qb = wu.qpart * nw + wave; qb < nqb; qb += qstep) {
-    int qrow[2];
-    bf16x8 qf[2][HD / 32];
+    const int qrow = qrown;
+    bf16x8 qf[NKK];
 #pragma unroll
-    for (int qh = 0; qh < 2; ++qh) {
-      qrow[qh] = qrown[qh];
+    for (int kk = 0; kk < NKK; ++kk) {
 #pragma unroll
-      for (int es = 0; es < HD / 32; ++es) qf[qh][es] = qfn[qh][es];
+      for (int j = 0; j < 8; ++j) qf[kk][j] = (__bf16)((float)qfn[kk][j] * qs);
     }
     load_q(min(qb + qstep, nqb - 1));
-    // the lane's table slots: [qt][kb][lane][8 floats], qt = 2 qb + qh
-    const f32x4* tq0 = reinterpret_cast<const f32x4*>(tch) + ((long)(qb * 2) * nkb * 64 + lane) * 2;
-    const long tqh = (long)nkb * 64 * 2;   // f32x4 stride between the two query halves
-    auto load_tab = [&](f32x4 (&s)[2][2], int kb) {
-#ifdef DFK_EXP_TABFIX
-      const f32x4* p = reinterpret_cast<const f32x4*>(tch) + lane * 2 + 0 * kb;
-#else
-      const f32x4* p = tq0 + (long)kb * 128;
-#endif
+    const bf16raw* tq0 = TAB ? tch + (long)qb * nkb * 1024 + lane * 8 : nullptr;   // 1024 bf16 per (qb, kb)
+    auto load_bias = [&](bf16x8 (&bt)[2], int kb) {
+      if constexpr (TAB) {
 #pragma unroll
-      for (int qh = 0; qh < 2; ++qh) {
-        s[qh][0] = p[qh * tqh];
-        s[qh][1] = p[qh * tqh + 1];
+        for (int c = 0; c < 2; ++c) bt[c] = *reinterpret_cast<const bf16x8*>(tq0 + (long)kb * 1024 + c * 512);
       }
     };
-    float m2[2] = {-INFINITY, -INFINITY};   // running max of S * scale * log2e
-    f32x4 o[2][HD / 16], lsum[2];
+    f32x16 o[NOT], mt;
+    f32x4 l4 = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = 0.f;
 #pragma unroll
-    for (int qh = 0; qh < 2; ++qh) {
-      lsum[qh] = f32x4{0, 0, 0, 0};
+    for (int j = 0; j < 16; ++j) mt[j] = 0.f;
 #pragma unroll
-      for (int et = 0; et < HD / 16; ++et) o[qh][et] = f32x4{0, 0, 0, 0};
-    }
-    // per key block: S = K Q^T onto the table tile (qk), softmax + O/l update (soft); the table tile of
-    // block kb+2 streams into the freed accumulators right after the exponentials
-    auto qk = [&](f32x4 (&s)[2][2], int kb) {
-      bf16x8 ka[2][HD / 32];
+    for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
+      for (int j = 0; j < 16; ++j) o[ot][j] = 0.f;
+    bf16x8 bt[2];
+    load_bias(bt, 0);
+    auto block = [&](int kb) {
+      // D = K Q'^T + bias' - m
+      f32x16 d;
 #pragma unroll
-        for (int es = 0; es < HD / 32; ++es)
-          ka[h2][es] = *reinterpret_cast<const bf16x8*>(Ks + swz<HD>(kb * 32 + h2 * 16 + ql, es * 32 + grp * 8));
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh)
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-          for (int es = 0; es < HD / 32; ++es)
-            s[qh][h2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[h2][es], qf[qh][es], s[qh][h2], 0, 0, 0);
-    };
-    auto soft = [&](f32x4 (&s)[2][2], int kb) {
-      bool grow = false;
-      float mnew[2];
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh) {
-        const float x0 = max3f(s[qh][0][0], s[qh][0][1], s[qh][0][2]);
-        const float x1 = max3f(s[qh][0][3], s[qh][1][0], s[qh][1][1]);
-        const float x2 = max3f(s[qh][1][2], s[qh][1][3], x0);
-#ifdef DFK_EXP_NOMAX
-        const float mx = 0.f * (x1 + x2);
-#else
-        const float mx = grp_max4(fmaxf(x1, x2)) * scale2;
-#endif
-        mnew[qh] = mx > m2[qh] + kRescale ? mx : m2[qh];
-        grow |= mnew[qh] != m2[qh];
+      for (int kk = 0; kk < NKK; ++kk) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + swz<HD>(kb * 32 + r, kk * 16 + hh * 8));
+        d = mfma32(kf, qf[kk], kk == 0 ? mt : d);
       }
+      if constexpr (TAB) {
+        d = mfma32(bt[0], id0, d);
+        d = mfma32(bt[1], id1, d);
+        load_bias(bt, min(kb + 1, nkb - 1));   // next block's tile: in flight under this block's softmax and PV
+      } else {
+        if (kb == nkb - 1) {   // keys beyond N (no table: the only padded key block)
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            if (kb * 32 + (j & 3) + 8 * (j >> 2) + 4 * hh >= g.N) d[j] = -INFINITY;
+        }
+      }
+      // lazy rescale: the block max relative to m (lanes l and l^32 hold the same query)
+      float x0 = max3f(d[0], d[1], d[2]), x1 = max3f(d[3], d[4], d[5]), x2 = max3f(d[6], d[7], d[8]);
+      float x3 = max3f(d[9], d[10], d[11]), x4 = max3f(d[12], d[13], d[14]);
+      float bm = max3f(max3f(x0, x1, x2), max3f(x3, x4, d[15]), -INFINITY);
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(bm), __float_as_uint(bm), false, false);
+      bm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      const bool grow = kb == 0 || bm > kRescale;
       if (__builtin_amdgcn_ballot_w64(grow) != 0) {
+        const float delta = grow ? bm : 0.f;
+        const float alpha = kb == 0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
+        m += delta;
 #pragma unroll
-        for (int qh = 0; qh < 2; ++qh) {
-          const float alpha = m2[qh] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m2[qh] - mnew[qh]);
-          m2[qh] = mnew[qh];
-          lsum[qh] *= alpha;
+        for (int j = 0; j < 16; ++j) { d[j] -= delta; mt[j] = -m; }
+        // the row sums sit in lanes 0-15 (queries 0-15 in register 0, 16-31 in register 1): their factors
+        const float a0 = __shfl(alpha, lane & 15, 64), a1 = __shfl(alpha, (lane & 15) + 16, 64);
+        l4[0] *= a0;
+        l4[1] *= a1;
 #pragma unroll
-          for (int et = 0; et < HD / 16; ++et) o[qh][et] *= alpha;
+        for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) o[ot][j] *= alpha;
+      }
+      // P = 2^D as the B operand of k-steps c = 0, 1 (registers 8c .. 8c+7)
+      bf16x8 pf[2], pv[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[c][j] = (__bf16)__builtin_amdgcn_exp2f(d[8 * c + j]);
+      if constexpr (DROP) {   // O accumulates the dropped probabilities, l the undropped ones
+        const long qrow_id = unit * g.Np + qb * 32 + r;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            pv[c][j] = (__bf16)((float)pf[c][j] * drop_mul(dc, qrow_id, kb * 32 + 16 * c + 8 * (j >> 2) + 4 * hh + (j & 3)));
+      } else {
+        pv[0] = pf[0];
+        pv[1] = pf[1];
+      }
+      // O^T += V^T P^T: A operand rows e = 32 ot + r, k-step c slots 8 hh + j <-> keys 16 c + 8 (j>>2) + 4 hh + (j&3)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int k0 = kb * 32 + 16 * c + 4 * (g16 >> 1) + tq;
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot) {
+          const int col = ot * 32 + 16 * (g16 & 1) + 4 * tp;
+          const bf16x8 va = tr16x2(Vs + swz<HD>(k0, col), Vs + swz<HD>(k0 + 8, col));
+          o[ot] = mfma32(va, pv[c], o[ot]);
         }
+        l4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf[c], l4, 0, 0, 0);
       }
-      bf16x8 pf[2];
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh)
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#ifdef DFK_EXP_NOEXP
-            pf[qh][h2 * 4 + r] = (__bf16)(__builtin_fmaf(s[qh][h2][r], scale2, -m2[qh]));
-#else
-            pf[qh][h2 * 4 + r] = (__bf16)__builtin_amdgcn_exp2f(__builtin_fmaf(s[qh][h2][r], scale2, -m2[qh]));
-#endif
-      load_tab(s, min(kb + 2, nkb - 1));   // unconditional (clamped): static vmcnt counts, no phi copies
-      // DROP: O accumulates the dropped probabilities, the denominator l the undropped ones
-      bf16x8 pv[2] = {pf[0], pf[1]};
-      if constexpr (DROP) {
-#pragma unroll
-        for (int qh = 0; qh < 2; ++qh) {
-          const long qrow_id = unit * g.Np + qb * 32 + qh * 16 + ql;
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              pv[qh][h2 * 4 + r] = (__bf16)((float)pf[qh][h2 * 4 + r] *
-                                            drop_mul(dc, qrow_id, kb * 32 + h2 * 16 + grp * 4 + r));
-        }
-      }
-#pragma unroll
-      for (int et = 0; et < HD / 16; ++et) {
-        const int c = et * 16 + tp * 4;
-        const bf16x8 va = tr16x2(Vs + swz<HD>(kb * 32 + grp * 4 + tq, c), Vs + swz<HD>(kb * 32 + 16 + grp * 4 + tq, c));
-#pragma unroll
-        for (int qh = 0; qh < 2; ++qh) o[qh][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pv[qh], o[qh][et], 0, 0, 0);
-      }
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh) lsum[qh] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qh], lsum[qh], 0, 0, 0);
     };
-    f32x4 sA[2][2], sB[2][2];
-    load_tab(sA, 0);
-    load_tab(sB, min(1, nkb - 1));
-    int kb = 0;
-    for (; kb + 1 < nkb; kb += 2) {
-      qk(sA, kb);
-      soft(sA, kb);
-      qk(sB, kb + 1);
-      soft(sB, kb + 1);
-    }
-    if (kb < nkb) {
-      qk(sA, kb);
-      soft(sA, kb);
-    }
+    for (int kb = 0; kb < nkb; ++kb) block(kb);
+    // O = O^T / l: lane holds e = 32 ot + (j & 3) + 8 (j >> 2) + 4 hh of query r
+    const float l = selsum(l4, lane);
+    const float inv = 1.f / l;
+    if (qrow >= 0) {
+      bf16raw* op = reinterpret_cast<bf16raw*>(a.out) + (long)qrow * a.ld_out + hoff;
 #pragma unroll
-    for (int qh = 0; qh < 2; ++qh) {
-      const int q = qb * 32 + qh * 16 + ql;
-      const float l = lsum[qh][0];
-      const float inv = 1.f / l;
-      if (qrow[qh] >= 0) {
-        bf16raw* op = reinterpret_cast<bf16raw*>(a.out) + (long)qrow[qh] * a.ld_out + hoff;
+      for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-        for (int et = 0; et < HD / 16; ++et) {
+        for (int jg = 0; jg < 4; ++jg) {
           uint2 u;
-          u.x = (uint32_t)f2bf(o[qh][et][0] * inv) | ((uint32_t)f2bf(o[qh][et][1] * inv) << 16);
-          u.y = (uint32_t)f2bf(o[qh][et][2] * inv) | ((uint32_t)f2bf(o[qh][et][3] * inv) << 16);
-          *reinterpret_cast<uint2*>(op + et * 16 + grp * 4) = u;
+          u.x = (uint32_t)f2bf(o[ot][4 * jg] * inv) | ((uint32_t)f2bf(o[ot][4 * jg + 1] * inv) << 16);
+          u.y = (uint32_t)f2bf(o[ot][4 * jg + 2] * inv) | ((uint32_t)f2bf(o[ot][4 * jg + 3] * inv) << 16);
+          *reinterpret_cast<uint2*>(op + ot * 32 + 8 * jg + 4 * hh) = u;
         }
-      }
-      if (a.lse && grp == 0 && q < g.N) a.lse[unit * g.Np + q] = (m2[qh] + __log2f(l)) * 0.6931471805599453f;
     }
+    const int q = qb * 32 + r;
+    if (a.lse && hh == 0 && q < g.N) a.lse[unit * g.Np + q] = (m + __log2f(l)) * 0.6931471805599453f;
   }
 }
 
@@ -926,11 +934,10 @@ extern "C" int dfk_wattn_table(const dfk_wattn_args* ap, hipStream_t s) {
   const dfk_wattn_args& a = *ap;
   const Geo g = make_geo(a);
   const TabGeo tg = tab_geo(a, g);
-  float* tf = reinterpret_cast<float*>(a.tab);
-  const long slots = tg.per_ch / 8 + tg.per_ch / 16;   // fwd + bwd layouts
-  hipLaunchKernelGGL(wattn_tab_kernel, dim3((unsigned)std::min<long>(dfk_cdiv(slots, 256), 64), tg.ncls * a.heads),
-                     dim3(256), 4 * (size_t)(g.Np + g.L), s, a, g, tg.per_ch / 8, tg.per_ch / 16, tf,
-                     tf + tab_elems(a, g));
+  bf16raw* t3 = tab3_fwd(a, g);
+  hipLaunchKernelGGL(wattn_tab3_kernel, dim3((unsigned)std::min<long>(dfk_cdiv(2 * tg.per_ch / 8, 256), 64),
+                                             tg.ncls * a.heads),
+                     dim3(256), 4 * (size_t)(g.Np + g.L), s, a, g, t3, t3 + tab_elems(a, g));
   DFK_CHECK_LAUNCH();
   return 0;
 }
@@ -939,30 +946,37 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
   if (!ap || !args_ok(*ap)) return DFK_EINVAL;
   const dfk_wattn_args& a = *ap;
   const Geo g = make_geo(a);
-  if (a.drop.mode && !(a.dtype == DFK_BF16 && a.tab && !a.mask && a.scale > 0.f)) return DFK_EINVAL;  // table path only
-  if (a.dtype == DFK_BF16 && a.tab && !a.mask && a.scale > 0.f) {   // table built by dfk_wattn_table
+  if (a.drop.mode && !(a.dtype == DFK_BF16 && !a.mask && a.scale > 0.f)) return DFK_EINVAL;  // bf16 v3 path only
+  if (a.dtype == DFK_BF16 && !a.mask && a.scale > 0.f && (a.tab || (!a.rpb && !g.use_mask))) {
+    // v3: bias tiles from dfk_wattn_table (RPB and / or shift mask), or no bias at all
     const long units = (long)a.B * g.nW * a.heads;
     if (units <= 0) return 0;
-    const float* tf = reinterpret_cast<const float*>(a.tab);
+    const bool tab = a.rpb || g.use_mask;
+    const bf16raw* t3 = tab ? tab3_fwd(a, g) : nullptr;
     const size_t lds = 4 * (size_t)g.Np * a.hd;
+    if (lds > 160 * 1024) return DFK_EINVAL;
     const int nqb = g.Np / 32;
     const int nw = std::min(4, nqb);
     const int qsplit = (int)std::max<long>(1, std::min<long>(dfk_cdiv(nqb, nw), dfk_cdiv(1024, units)));
     dim3 grid((unsigned)(units * qsplit));
-#define LAUNCH_T(HD, DR)                                                                                     \
+#define LAUNCH_3(HD, TB, DR)                                                                                 \
   do {                                                                                                       \
-    auto kfn = wattn_fwd_tab_kernel<HD, DR>;                                                                 \
+    auto kfn = wattn_fwd3_kernel<HD, TB, DR>;                                                                \
     static bool attr_set = false;                                                                            \
     if (!attr_set) {                                                                                         \
       (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);   \
       attr_set = true;                                                                                       \
     }                                                                                                        \
-    hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), lds, s, a, g, qsplit, (const float*)tf);                 \
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), lds, s, a, g, qsplit, t3);                                 \
   } while (0)
-    const bool dr = a.drop.mode != 0;
-    if (a.hd == 32) { if (dr) LAUNCH_T(32, true); else LAUNCH_T(32, false); }
-    else { if (dr) LAUNCH_T(64, true); else LAUNCH_T(64, false); }
-#undef LAUNCH_T
+#define PICK_3(HD)                                                                       \
+  do {                                                                                   \
+    if (tab) { if (a.drop.mode) LAUNCH_3(HD, true, true); else LAUNCH_3(HD, true, false); } \
+    else { if (a.drop.mode) LAUNCH_3(HD, false, true); else LAUNCH_3(HD, false, false); }   \
+  } while (0)
+    if (a.hd == 32) PICK_3(32); else PICK_3(64);
+#undef PICK_3
+#undef LAUNCH_3
     DFK_CHECK_LAUNCH();
     return 0;
   }
@@ -1338,13 +1352,10 @@ __global__ __launch_bounds__(256) void wattn_bwd_kernel(const dfk_wattn_bwd_args
 // from XOR-swizzled tiles, dS crossing the wave's scratch as dS^T (b64 stores,
 // tr16 loads), and a bank-swizzled dQ accumulator.
 
-// TAB: the score bias (RPB + shift mask, -inf beyond N) comes from the forward's bwd-layout table as the
-// C input of S = Q K^T (no per-score gather, label compare or key mask).
-template <int HD, bool RPB, bool MASK, bool TAB = false, bool DROP = false>
+template <int HD, bool RPB, bool MASK>
 __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(const dfk_wattn_bwd_args ba, const Geo g,
                                                                               int q0, int Qn, int accum_kv,
-                                                                              bf16raw* __restrict__ dsg,
-                                                                              const float* __restrict__ tabb) {
+                                                                              bf16raw* __restrict__ dsg) {
   // One workgroup = one (clip, window, head); wave w owns key blocks w, w + nwaves (dK, dV in registers).
   // All waves step through the query blocks together: per 32-query block each wave computes S, dP, P, dS
   // for its keys, accumulates dV += P^T dO and dK += dS^T Q, and its partial dQ = dS K; the partials are
@@ -1374,9 +1385,6 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
   const int win = unit % g.nW, b = unit / g.nW;
   const float* mrow = MASK ? a.mask + (((long)b * g.nW + win) % a.mask_nw) * g.N * g.N : nullptr;
   const int hoff = head * HD;
-  const f32x4* tch = TAB ? reinterpret_cast<const f32x4*>(tabb) +
-                               ((long)win_class(a, g, win) * a.heads + head) * (long)g.Np * g.Np / 4 + lane * 4
-                         : nullptr;
   const bf16raw* og = reinterpret_cast<const bf16raw*>(a.out);
   const bf16raw* dog = reinterpret_cast<const bf16raw*>(ba.dout);
   const bf16raw* qg = reinterpret_cast<const bf16raw*>(a.q);
@@ -1421,7 +1429,6 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
   float* myQ = dQp + wave * 32 * kDqStride;
   const float scale2 = a.scale * kLog2e;
   const float mpen = -100.f * kLog2e;
-  const DropCtx dc = drop_ctx(a.drop);   // DROP: the forward's attention-dropout mask (row = unit*Np + q, col = k)
   bf16raw* dsu = RPB && dsg ? dsg + (long)blockIdx.x * g.Np * g.Np : nullptr;   // this window-head's dS^T [k][q]
   for (int pass = 0; pass * nwaves < nkb; ++pass) {
     const int kb = pass * nwaves + wave;
@@ -1480,28 +1487,20 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
           }
         }
         float bias[2][2][4];
-        f32x4 tb[2][2];
-        if constexpr (TAB) {   // table tile (query block, key block): 4 x 16 B per lane
-          const f32x4* tp4 = tch + ((long)((q0 + qr0) / 32) * (g.Np / 32) + kb) * 256;
-#pragma unroll
-          for (int qh = 0; qh < 2; ++qh)
-#pragma unroll
-            for (int h2 = 0; h2 < 2; ++h2) tb[qh][h2] = tp4[qh * 2 + h2];
-        }
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh)
 #pragma unroll
           for (int h2 = 0; h2 < 2; ++h2)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              bias[qh][h2][r] = RPB && !TAB ? rpb2[(QP[qh][r] >> 5) - (kpk[h2] >> 5) + g.C0] : 0.f;
+              bias[qh][h2][r] = RPB ? rpb2[(QP[qh][r] >> 5) - (kpk[h2] >> 5) + g.C0] : 0.f;
         // S = Q K^T, dP = dO V^T : rows = queries, lanes = keys
         f32x4 s[2][2], dp[2][2];
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh)
 #pragma unroll
           for (int h2 = 0; h2 < 2; ++h2) {
-            s[qh][h2] = TAB ? tb[qh][h2] : f32x4{0, 0, 0, 0};
+            s[qh][h2] = f32x4{0, 0, 0, 0};
             dp[qh][h2] = f32x4{0, 0, 0, 0};
 #pragma unroll
             for (int es = 0; es < HD / 32; ++es) {
@@ -1518,24 +1517,15 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
             float dsv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float x;
-              if constexpr (TAB) {
-                x = __builtin_fmaf(s[qh][h2][r], scale2, -L2[qh][r]);
-              } else {
-                x = s[qh][h2][r] * scale2 + (bias[qh][h2][r] + kneg[h2] - L2[qh][r]);
-                if (g.use_mask) x += ((QP[qh][r] ^ kpk[h2]) & 31) ? mpen : 0.f;
-              }
+              float x = s[qh][h2][r] * scale2 + (bias[qh][h2][r] + kneg[h2] - L2[qh][r]);
+              if (g.use_mask) x += ((QP[qh][r] ^ kpk[h2]) & 31) ? mpen : 0.f;
               if constexpr (MASK) {
                 const int q = q0 + qr0 + qh * 16 + grp * 4 + r, k = kb * 32 + h2 * 16 + ql;
                 if (q < g.N && k < g.N) x += mrow[q * g.N + k] * kLog2e;
               }
               const float P = __builtin_amdgcn_exp2f(x);
-              float mk = 1.f;
-              if constexpr (DROP)
-                mk = drop_mul(dc, (long)blockIdx.x * g.Np + q0 + qr0 + qh * 16 + grp * 4 + r, kb * 32 + h2 * 16 + ql);
-              // dropout: dV = (P.Z/keep)^T dO, dS = P (dP.Z/keep - rowsum(dO.O)) with O the dropped output
-              const float dS = P * (dp[qh][h2][r] * mk - DL[qh][r]);
-              pa[h2][qh * 4 + r] = (__bf16)(P * mk);
+              const float dS = P * (dp[qh][h2][r] - DL[qh][r]);
+              pa[h2][qh * 4 + r] = (__bf16)P;
               sa[h2][qh * 4 + r] = (__bf16)dS;
               dsv[r] = dS;
             }
@@ -1638,278 +1628,272 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
   }
 }
 
-// Backward with the bias tables, one launch over all Np queries of the window (Q, dO resident in LDS).
-// One workgroup = one (clip, window, head); wave w owns key blocks w, w + nwaves (dK, dV in registers) and
-// sweeps every query block, STAGGERED: at step i wave w takes query block (i + w) mod nqb, so at any step the
-// waves touch distinct query blocks of the fp32 dQ accumulator in LDS and add their partial dQ = dS K into it
-// with a plain read-add-write; one barrier per step keeps the waves in step, so the add order per element is
-// fixed (deterministic).  (LDS float atomics instead of the barrier measured 3x slower.)  The table tile of the next step is
-// loaded one step ahead; no global read-modify-write inside the sweep.  dS^T still goes to the global
-// scratch (dsg) for the dRPB reduction.
-template <int HD, bool DROP>
-__global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_tab_kernel(const dfk_wattn_bwd_args ba, const Geo g,
-                                                            bf16raw* __restrict__ dsg,
-                                                            const float* __restrict__ tabb) {
+// ------------------------------------------------- v3 backward (bf16 bias tiles, 32x32x16 MFMA)
+// One workgroup = one (clip, window, head); wave w owns key blocks w, w + nw, ... (dK^T, dV^T in registers) and
+// sweeps every query block STAGGERED (wave w at step i takes block (i + w) mod nqb), so at each step the waves
+// add their partial dQ = dS K into distinct blocks of the fp32 LDS accumulator, behind one barrier per step (a
+// fixed add order: deterministic).  Per step (32 queries x 32 keys, queries on the MFMA row, keys on the lane):
+//   S' = Q' K^T + bias' - L'   (Q' = Q scale log2e, staged so in LDS; -L' = -lse log2e enters as the C input,
+//                               read from LDS; bias' by the identity product of the forward, bwd tile layout)
+//   dP' = dO V^T - delta        (-delta as the C input; delta = rowsum(dO O))
+//   P = 2^S', dS = P dP'        (dropout: dS = P (dP Z/keep - delta), P Z/keep into dV)
+//   dV^T += dO^T P, dK^T += Q'^T dS  (the score accumulators are the B operands: no lane movement)
+//   dQ_part = dS K              (dS crosses the wave's LDS scratch once, as dS^T, read back transposed)
+// dS^T also goes to the global scratch (dsg) for the deterministic dRPB reduction.
+constexpr int kSdRow = 32;   // bf16 per row of the [32 keys][32 queries] dS^T scratch (64 B)
+
+// element (k, q) of the dS^T scratch: 8-B column groups XOR-swizzled by k so that the packed stores (4 x 16 lanes,
+// bank (a/4) mod 32) and the tr16 reads (2 x 32 lanes, mod 64) are conflict-free
+__device__ __forceinline__ int sd_off(int k, int q) { return k * kSdRow + ((((q >> 2) ^ (k >> 1)) & 7) << 2) + (q & 3); }
+
+template <int HD, bool TAB, bool DROP>
+__global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_args ba, const Geo g,
+                                                         bf16raw* __restrict__ dsg, const bf16raw* __restrict__ tabb) {
+  constexpr int NKK = HD / 16, NOT = HD / 32, CH = HD / 8;
   const dfk_wattn_args& a = ba.f;
-  const int nwaves = blockDim.x >> 6;
+  const int nw = blockDim.x >> 6;
   const int Np = g.Np, nkb = Np / 32, nqb = Np / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* p = smem;
-  float* dQa = reinterpret_cast<float*>(p); p += 4 * (size_t)Np * HD;   // per 32-query block: [qh][et][lane][4]
-  bf16raw* Qs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;
+  float* dQa = reinterpret_cast<float*>(p); p += 4 * (size_t)Np * HD;   // [qb][ot][v][lane][4]
+  bf16raw* Qs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;  // Q' = Q scale log2e
   bf16raw* dOs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;
-  bf16raw* Sd = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)nwaves * 32 * kSdStride;
+  bf16raw* Sd = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)nw * 32 * kSdRow;
   int* trow = reinterpret_cast<int*>(p); p += 4 * Np;
-  float* lse2 = reinterpret_cast<float*>(p); p += 4 * Np;   // lse * log2(e); +inf beyond N
-  float* delta = reinterpret_cast<float*>(p);
+  float* nl2 = reinterpret_cast<float*>(p); p += 4 * Np;   // -lse log2e; -inf beyond N (P = 0)
+  float* ndl = reinterpret_cast<float*>(p); p += 4 * Np;   // -delta
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int grp = lane >> 4, ql = lane & 15, tq = ql >> 2, tp = ql & 3;
+  const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   int unit = blockIdx.x;
   const int head = unit % a.heads;
   unit /= a.heads;
   const int win = unit % g.nW, b = unit / g.nW;
   const int hoff = head * HD;
-  const f32x4* tch = reinterpret_cast<const f32x4*>(tabb) +
-                     ((long)win_class(a, g, win) * a.heads + head) * (long)Np * Np / 4 + lane * 4;
+  const bf16raw* tch = TAB ? tabb + ((long)win_class(a, g, win) * a.heads + head) * (long)Np * Np + lane * 8 : nullptr;
+  const float qs = a.scale * kLog2e;
 
   for (int i = tid; i < Np; i += blockDim.x) {
     trow[i] = token_info_row(a, g, b, win, i);
-    lse2[i] = i < g.N ? a.lse[(long)blockIdx.x * Np + i] * kLog2e : INFINITY;
+    nl2[i] = i < g.N ? -a.lse[(long)blockIdx.x * Np + i] * kLog2e : -INFINITY;
   }
   for (int i = tid * 4; i < Np * HD; i += blockDim.x * 4) *reinterpret_cast<f32x4*>(dQa + i) = f32x4{0, 0, 0, 0};
   __syncthreads();
-  constexpr int CH = HD / 8;
   for (int base = 0; base < Np * CH; base += blockDim.x) {
     const int idx = base + tid;
     float d = 0.f;
     if (idx < Np * CH) {
       const int li = idx / CH, c = (idx % CH) * 8;
       const int row = trow[li];
-      const uint4 qv = tok_ld16<bf16raw>(a.q, a.pad_q, row, a.ld_qkv, hoff + c);
+      uint4 qv = tok_ld16<bf16raw>(a.q, a.pad_q, row, a.ld_qkv, hoff + c);
       const uint4 dv = tok_ld16<bf16raw>(ba.dout, nullptr, row, ba.ld_dout, hoff + c);
       const uint4 ov = tok_ld16<bf16raw>(a.out, nullptr, row, a.ld_out, hoff + c);
       d = dot8_bf16(ov, dv);
-      *reinterpret_cast<uint4*>(Qs + swz<HD>(li, c)) = qv;
+      bf16x8 qb8 = __builtin_bit_cast(bf16x8, qv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qb8[j] = (__bf16)((float)qb8[j] * qs);   // the forward's Q' rounding, bit for bit
+      *reinterpret_cast<bf16x8*>(Qs + swz<HD>(li, c)) = qb8;
       *reinterpret_cast<uint4*>(dOs + swz<HD>(li, c)) = dv;
     }
 #pragma unroll
     for (int o = 1; o < CH; o <<= 1) d += __shfl_xor(d, o, 64);
-    if (idx < Np * CH && (idx % CH) == 0) delta[idx / CH] = d;
+    if (idx < Np * CH && (idx % CH) == 0) ndl[idx / CH] = -d;
   }
   __syncthreads();
 
-  bf16raw* Sw = Sd + wave * 32 * kSdStride;
-  const float scale2 = a.scale * kLog2e;
+  bf16x8 id0, id1, sel;
+  bias_ident(lane, id0, id1, sel);
+  bf16raw* Sw = Sd + wave * 32 * kSdRow;
   const DropCtx dc = drop_ctx(a.drop);
   bf16raw* dsu = dsg ? dsg + (long)blockIdx.x * Np * Np : nullptr;   // this window-head's dS^T [k][q]
-  for (int pass = 0; pass * nwaves < nkb; ++pass) {
-    const int kb = pass * nwaves + wave;
+  for (int pass = 0; pass * nw < nkb; ++pass) {
+    const int kb = pass * nw + wave;
     if (kb >= nkb) {   // no key block this pass: keep the step barriers
-#ifndef DFK_EXP_NOBAR
       for (int i = 0; i < nqb; ++i) __syncthreads();
-#endif
       continue;
     }
-    bf16x8 kB[2][HD / 32], vB[2][HD / 32], kN[HD / 16];
-    f32x4 dK[2][HD / 16], dV[2][HD / 16];
+    // K^T / V^T B operands (key on the lane) and K as the B operand of dQ = dS K (e on the lane)
+    const int krow = trow[kb * 32 + r];
+    const float kneg = kb * 32 + r < g.N ? 0.f : -INFINITY;   // keys beyond N (the bias tiles also hold -1e4 there)
+    bf16x8 kB[NKK], vB[NKK], kN[2][NOT];
 #pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      const int row = trow[kb * 32 + h2 * 16 + ql];
+    for (int kk = 0; kk < NKK; ++kk) {
+      kB[kk] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.k, a.pad_k, krow, a.ld_qkv, hoff + kk * 16 + hh * 8));
+      vB[kk] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.v, a.pad_v, krow, a.ld_qkv, hoff + kk * 16 + hh * 8));
+    }
 #pragma unroll
-      for (int es = 0; es < HD / 32; ++es) {
-        kB[h2][es] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + es * 32 + grp * 8));
-        vB[h2][es] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + es * 32 + grp * 8));
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = trow[kb * 32 + 16 * s + 8 * hh + j];
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot)
+          kN[s][ot][j] = __builtin_bit_cast(__bf16, tok_ld1<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + ot * 32 + r));
       }
+    f32x16 dKt[NOT], dVt[NOT];
 #pragma unroll
-      for (int et = 0; et < HD / 16; ++et) { dK[h2][et] = f32x4{0, 0, 0, 0}; dV[h2][et] = f32x4{0, 0, 0, 0}; }
-    }
+    for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int row = trow[kb * 32 + grp * 8 + j];
+      for (int j = 0; j < 16; ++j) { dKt[ot][j] = 0.f; dVt[ot][j] = 0.f; }
+    bf16x8 bt[2];
+    auto load_bias = [&](int qb) {
+      if constexpr (TAB) {
 #pragma unroll
-      for (int et = 0; et < HD / 16; ++et)
-        kN[et][j] = __builtin_bit_cast(__bf16, tok_ld1<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + ql + et * 16));
-    }
-    auto tab_tile = [&](f32x4 (&t)[2][2], int qb) {
-#ifdef DFK_EXP_TABFIX
-      const f32x4* tp4 = tch + 0 * qb;
-#else
-      const f32x4* tp4 = tch + ((long)qb * nkb + kb) * 256;
-#endif
-#pragma unroll
-      for (int qh = 0; qh < 2; ++qh)
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) t[qh][h2] = tp4[qh * 2 + h2];
+        for (int c = 0; c < 2; ++c)
+          bt[c] = *reinterpret_cast<const bf16x8*>(tch + ((long)(qb * nkb + kb) * 2 + c) * 512);
+      }
     };
-    auto nxt = [&](int q) { return q + 1 == nqb ? 0 : q + 1; };
-    // one step: query block qb against the owned key block; t holds the block's table tile on entry and
-    // receives the tile of the block three steps ahead (loaded once the scores have left it)
-    auto step = [&](f32x4 (&t)[2][2], int qb) {
-      const int qr0 = qb * 32;
-      f32x4 L2[2], DL[2];
-      bf16x8 qa[2][HD / 32], da[2][HD / 32];
+    int qb = wave % nqb;
+    load_bias(qb);
+    for (int i = 0; i < nqb; ++i, qb = qb + 1 == nqb ? 0 : qb + 1) {
+      const int q0 = qb * 32;
+      // row constants as the C inputs: queries q0 + 8 v + 4 hh + (0..3) in registers 4v .. 4v+3
+      f32x16 s, dp;
 #pragma unroll
-      for (int qh = 0; qh < 2; ++qh) {
-        const int r0 = qr0 + qh * 16 + grp * 4;
-        L2[qh] = *reinterpret_cast<const f32x4*>(lse2 + r0);
-        DL[qh] = *reinterpret_cast<const f32x4*>(delta + r0);
+      for (int v = 0; v < 4; ++v) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(nl2 + q0 + 8 * v + 4 * hh);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(ndl + q0 + 8 * v + 4 * hh);
 #pragma unroll
-        for (int es = 0; es < HD / 32; ++es) {
-          const int off = swz<HD>(qr0 + qh * 16 + ql, es * 32 + grp * 8);
-          qa[qh][es] = *reinterpret_cast<const bf16x8*>(Qs + off);
-          da[qh][es] = *reinterpret_cast<const bf16x8*>(dOs + off);
+        for (int t = 0; t < 4; ++t) {
+          s[4 * v + t] = l4[t] + kneg;
+          dp[4 * v + t] = DROP ? 0.f : d4[t];
         }
       }
-      // S = Q K^T (+ table), dP = dO V^T : rows = queries, lanes = keys
-      f32x4 dp[2][2];
 #pragma unroll
-      for (int qh = 0; qh < 2; ++qh)
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          dp[qh][h2] = f32x4{0, 0, 0, 0};
-#pragma unroll
-          for (int es = 0; es < HD / 32; ++es) {
-            t[qh][h2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[qh][es], kB[h2][es], t[qh][h2], 0, 0, 0);
-            dp[qh][h2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[qh][es], vB[h2][es], dp[qh][h2], 0, 0, 0);
-          }
-        }
-      // P = 2^(s*scale*log2e - lse2); dS = P (dP - delta)
+      for (int kk = 0; kk < NKK; ++kk) {
+        const int off = swz<HD>(q0 + r, kk * 16 + hh * 8);
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + off);
+        const bf16x8 da = *reinterpret_cast<const bf16x8*>(dOs + off);
+        s = mfma32(qa, kB[kk], s);
+        dp = mfma32(da, vB[kk], dp);
+      }
+      if constexpr (TAB) {
+        s = mfma32(bt[0], id0, s);
+        s = mfma32(bt[1], id1, s);
+        load_bias(qb + 1 == nqb ? 0 : qb + 1);
+      }
+      // P = 2^S', dS = P dP'; B-operand fragments of k-steps c (registers 8c .. 8c+7)
       bf16x8 pa[2], sa[2];
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int qh = 0; qh < 2; ++qh)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float P = __builtin_amdgcn_exp2f(__builtin_fmaf(t[qh][h2][r], scale2, -L2[qh][r]));
-            float mk = 1.f;
-            if constexpr (DROP)
-              mk = drop_mul(dc, (long)blockIdx.x * Np + qr0 + qh * 16 + grp * 4 + r, kb * 32 + h2 * 16 + ql);
-            pa[h2][qh * 4 + r] = (__bf16)(P * mk);
-            sa[h2][qh * 4 + r] = (__bf16)(P * (dp[qh][h2][r] * mk - DL[qh][r]));
+        for (int j = 0; j < 8; ++j) {
+          const float P = __builtin_amdgcn_exp2f(s[8 * c + j]);
+          if constexpr (DROP) {
+            const int q = q0 + 8 * (2 * c + (j >> 2)) + 4 * hh + (j & 3);
+            const float mk = drop_mul(dc, (long)blockIdx.x * Np + q, kb * 32 + r);
+            pa[c][j] = (__bf16)(P * mk);
+            sa[c][j] = (__bf16)(P * (dp[8 * c + j] * mk + ndl[q]));
+          } else {
+            pa[c][j] = (__bf16)P;
+            sa[c][j] = (__bf16)(P * dp[8 * c + j]);
           }
-      tab_tile(t, nxt(nxt(nxt(qb))));   // three steps ahead, before this step's scratch stores (vmcnt order)
-      // dS^T -> wave scratch [32 keys][32 queries] (the bf16 bits of the A operand)
+        }
+      // dS^T -> the wave's scratch: registers 4v .. 4v+3 (queries 8v + 4hh + 0..3) at [key r][8v + 4hh]
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const uint4 u = __builtin_bit_cast(uint4, sa[h2]);
-        *reinterpret_cast<uint2*>(Sw + (h2 * 16 + ql) * kSdStride + grp * 4) = make_uint2(u.x, u.y);
-        *reinterpret_cast<uint2*>(Sw + (h2 * 16 + ql) * kSdStride + 16 + grp * 4) = make_uint2(u.z, u.w);
+      for (int c = 0; c < 2; ++c) {
+        const uint4 u = __builtin_bit_cast(uint4, sa[c]);
+        *reinterpret_cast<uint2*>(Sw + sd_off(r, 16 * c + 4 * hh)) = make_uint2(u.x, u.y);
+        *reinterpret_cast<uint2*>(Sw + sd_off(r, 16 * c + 8 + 4 * hh)) = make_uint2(u.z, u.w);
       }
-      // dV[k][e] += P^T dO ; dK[k][e] += dS^T Q   (query slot j <-> row qr0 + (j>>2)*16 + 4grp + (j&3))
+      // dV^T += dO^T P, dK^T += Q'^T dS: A rows e = 32 ot + r, k-step c slots <-> queries 16 c + 8 (j>>2) + 4 hh + (j&3)
 #pragma unroll
-      for (int et = 0; et < HD / 16; ++et) {
-        const int c = et * 16 + tp * 4;
-        const int rlo = qr0 + grp * 4 + tq, rhi = rlo + 16;
-        const bf16x8 dob = tr16x2(dOs + swz<HD>(rlo, c), dOs + swz<HD>(rhi, c));
-        const bf16x8 qbv = tr16x2(Qs + swz<HD>(rlo, c), Qs + swz<HD>(rhi, c));
+      for (int c = 0; c < 2; ++c) {
+        const int qr = q0 + 16 * c + 4 * (g16 >> 1) + tq;
 #pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          dV[h2][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[h2], dob, dV[h2][et], 0, 0, 0);
-          dK[h2][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa[h2], qbv, dK[h2][et], 0, 0, 0);
+        for (int ot = 0; ot < NOT; ++ot) {
+          const int col = ot * 32 + 16 * (g16 & 1) + 4 * tp;
+          const bf16x8 doT = tr16x2(dOs + swz<HD>(qr, col), dOs + swz<HD>(qr + 8, col));
+          const bf16x8 qT = tr16x2(Qs + swz<HD>(qr, col), Qs + swz<HD>(qr + 8, col));
+          dVt[ot] = mfma32(doT, pa[c], dVt[ot]);
+          dKt[ot] = mfma32(qT, sa[c], dKt[ot]);
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's own scratch writes (LDS only)
       __builtin_amdgcn_wave_barrier();
-      // partial dQ[q][e] = dS K over this key block (dS rows via tr16 from the scratch)
-      f32x4 dq[2][HD / 16];
+      // partial dQ = dS K: A = dS (row q = r, k-step s slots 8 hh + j <-> keys 16 s + 8 hh + j) read transposed
+      f32x16 dq[NOT];
 #pragma unroll
-      for (int qh = 0; qh < 2; ++qh) {
-        const bf16x8 sq = tr16x2(Sw + (grp * 8 + tq) * kSdStride + qh * 16 + tp * 4,
-                                 Sw + (grp * 8 + 4 + tq) * kSdStride + qh * 16 + tp * 4);
+      for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-        for (int et = 0; et < HD / 16; ++et)
-          dq[qh][et] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sq, kN[et], f32x4{0, 0, 0, 0}, 0, 0, 0);
+        for (int j = 0; j < 16; ++j) dq[ot][j] = 0.f;
+#pragma unroll
+      for (int sk = 0; sk < 2; ++sk) {
+        const int k0 = 16 * sk + 8 * (g16 >> 1) + tq, qc = 16 * (g16 & 1) + 4 * tp;
+        const bf16x8 dsa = tr16x2(Sw + sd_off(k0, qc), Sw + sd_off(k0 + 4, qc));
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot) dq[ot] = mfma32(dsa, kN[sk][ot], dq[ot]);
       }
-#ifdef DFK_EXP_NODS
-      if (false) {
-#else
-      if (dsu) {   // scratch rows (32 keys x 64 B) -> global dS^T[k][q], 2 x 16 B per lane
-#endif
+      if (dsu) {   // scratch rows (32 keys x 64 B) -> global dS^T[k][q]: lane (key kr, half) un-swizzles 2 x 16 B
         const int kr = lane >> 1, half = lane & 1;
-        const uint4 v0 = *reinterpret_cast<const uint4*>(Sw + kr * kSdStride + half * 16);
-        const uint4 v1 = *reinterpret_cast<const uint4*>(Sw + kr * kSdStride + half * 16 + 8);
-        bf16raw* gp = dsu + (long)(kb * 32 + kr) * Np + qr0 + half * 16;
-        *reinterpret_cast<uint4*>(gp) = v0;
-        *reinterpret_cast<uint4*>(gp + 8) = v1;
+        const uint2 x0 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16));
+        const uint2 x1 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 4));
+        const uint2 x2 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 8));
+        const uint2 x3 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 12));
+        bf16raw* gp = dsu + (long)(kb * 32 + kr) * Np + q0 + half * 16;
+        *reinterpret_cast<uint4*>(gp) = make_uint4(x0.x, x0.y, x1.x, x1.y);
+        *reinterpret_cast<uint4*>(gp + 8) = make_uint4(x2.x, x2.y, x3.x, x3.y);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before the next step's writes
       __builtin_amdgcn_wave_barrier();
-      float* acc = dQa + (size_t)qb * 32 * HD + lane * 4;
-#ifndef DFK_EXP_NOBAR
       __syncthreads();   // every wave has finished the previous step's adds: block qb is this wave's alone
-#endif
 #pragma unroll
-      for (int qh = 0; qh < 2; ++qh)
+      for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-        for (int et = 0; et < HD / 16; ++et) {
-          f32x4* ap = reinterpret_cast<f32x4*>(acc + (qh * (HD / 16) + et) * 256);
-          *ap = *ap + dq[qh][et];
+        for (int v = 0; v < 4; ++v) {
+          f32x4* ap = reinterpret_cast<f32x4*>(dQa + ((size_t)((qb * NOT + ot) * 4 + v) * 64 + lane) * 4);
+          *ap = *ap + f32x4{dq[ot][4 * v], dq[ot][4 * v + 1], dq[ot][4 * v + 2], dq[ot][4 * v + 3]};
         }
-    };
-    f32x4 tA[2][2], tB[2][2], tC[2][2];
-    int qb = wave % nqb;   // stagger: distinct query blocks per wave at every step (nwaves <= nqb)
-    tab_tile(tA, qb);
-    tab_tile(tB, nxt(qb));
-    tab_tile(tC, nxt(nxt(qb)));
-    int i = 0;
-    for (; i + 2 < nqb; i += 3) {
-      step(tA, qb);
-      qb = nxt(qb);
-      step(tB, qb);
-      qb = nxt(qb);
-      step(tC, qb);
-      qb = nxt(qb);
     }
-    if (i < nqb) step(tA, qb);
-    if (i + 1 < nqb) step(tB, nxt(qb));
-    // ---- dK (scaled), dV of the owned key block: C layout row = key 4grp+r, col = e
+    // dK = scale sum dS q = (sum dS Q') ln 2, dV: lane holds key r, e = 32 ot + (j & 3) + 8 (j >> 2) + 4 hh
+    const float kscale = 0.6931471805599453f;
 #pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2)
+    for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = trow[kb * 32 + h2 * 16 + grp * 4 + r];
+      for (int v = 0; v < 4; ++v) {
+        const int e = hoff + ot * 32 + 8 * v + 4 * hh;
+        if (krow >= 0) {
+          uint2 uk, uv;
+          uk.x = (uint32_t)f2bf(dKt[ot][4 * v] * kscale) | ((uint32_t)f2bf(dKt[ot][4 * v + 1] * kscale) << 16);
+          uk.y = (uint32_t)f2bf(dKt[ot][4 * v + 2] * kscale) | ((uint32_t)f2bf(dKt[ot][4 * v + 3] * kscale) << 16);
+          uv.x = (uint32_t)f2bf(dVt[ot][4 * v]) | ((uint32_t)f2bf(dVt[ot][4 * v + 1]) << 16);
+          uv.y = (uint32_t)f2bf(dVt[ot][4 * v + 2]) | ((uint32_t)f2bf(dVt[ot][4 * v + 3]) << 16);
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16raw*>(ba.dk) + (long)krow * ba.ld_dqkv + e) = uk;
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16raw*>(ba.dv) + (long)krow * ba.ld_dqkv + e) = uv;
+        } else if (krow == -1) {
 #pragma unroll
-        for (int et = 0; et < HD / 16; ++et) {
-          const int e = hoff + et * 16 + ql;
-          const float vk = dK[h2][et][r] * a.scale, vv = dV[h2][et][r];
-          if (row >= 0) {
-            reinterpret_cast<bf16raw*>(ba.dk)[(long)row * ba.ld_dqkv + e] = f2bf(vk);
-            reinterpret_cast<bf16raw*>(ba.dv)[(long)row * ba.ld_dqkv + e] = f2bf(vv);
-          } else if (row == -1) {
-            if (ba.dpad_k) atomicAdd(ba.dpad_k + e, vk);
-            if (ba.dpad_v) atomicAdd(ba.dpad_v + e, vv);
+          for (int t = 0; t < 4; ++t) {
+            if (ba.dpad_k) atomicAdd(ba.dpad_k + e + t, dKt[ot][4 * v + t] * kscale);
+            if (ba.dpad_v) atomicAdd(ba.dpad_v + e + t, dVt[ot][4 * v + t]);
           }
         }
       }
   }
   __syncthreads();
-  // ---- dQ rows (scaled) from the accumulator: element (q, e) of block qb sits at
-  //      [qb][qh][et][lane = 16 * grp + (e & 15)][r] with q = 32 qb + 16 qh + 4 grp + r, e = 16 et + (e & 15)
-  for (int t = tid; t < Np * (HD / 8); t += blockDim.x) {
-    const int i = t / (HD / 8), c = (t % (HD / 8)) * 8;
+  // dQ rows (scaled): (q, e) of block qb sits at [qb][ot][v][lane][t], q = 32 qb + 8 v + 4 h + t, lane = (e & 31) + 32 h
+  for (int t8 = tid; t8 < Np * (HD / 8); t8 += blockDim.x) {
+    const int i = t8 / (HD / 8), c = (t8 % (HD / 8)) * 8;
     const int row = i < g.N ? trow[i] : -2;
-    const int qb = i >> 5, qh = (i >> 4) & 1, gq = (i >> 2) & 3, r = i & 3, et = c >> 4;
-    const float* src = dQa + (size_t)qb * 32 * HD + (qh * (HD / 16) + et) * 256 + (gq * 16 + (c & 15)) * 4 + r;
-    float v[8];
+    const int qb = i >> 5, qi = i & 31, v = qi >> 3, h2 = (qi >> 2) & 1, t = qi & 3, ot = c >> 5;
+    const float* src = dQa + ((size_t)((qb * NOT + ot) * 4 + v) * 64 + (c & 31) + 32 * h2) * 4 + t;
+    float vv[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = src[j * 4] * a.scale;
+    for (int j = 0; j < 8; ++j) vv[j] = src[j * 4] * a.scale;
     if (row >= 0) {
       uint4 u;
       bf16raw* pe = reinterpret_cast<bf16raw*>(&u);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pe[j] = f2bf(v[j]);
+      for (int j = 0; j < 8; ++j) pe[j] = f2bf(vv[j]);
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16raw*>(ba.dq) + (long)row * ba.ld_dqkv + hoff + c) = u;
     } else if (row == -1 && ba.dpad_q) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(ba.dpad_q + hoff + c + j, v[j]);
+      for (int j = 0; j < 8; ++j) atomicAdd(ba.dpad_q + hoff + c + j, vv[j]);
     }
   }
 }
 
-size_t bwd_tab_lds(const dfk_wattn_args& a, const Geo& g, int nwaves) {
-  return 8 * (size_t)g.Np * a.hd + 2 * (size_t)nwaves * 32 * kSdStride + 12 * (size_t)g.Np;
+size_t bwd3_lds(const dfk_wattn_args& a, const Geo& g, int nw) {
+  return 8 * (size_t)g.Np * a.hd + 2 * (size_t)nw * 32 * kSdRow + 12 * (size_t)g.Np;
 }
 
 // dRPB from the dS^T scratch: drpb[pos(q) - pos(k) + C0] += sum over windows of dS[q][k].
@@ -1995,6 +1979,49 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
   const int vec = a.dtype == DFK_BF16 ? 8 : 4;
   if (bp->ld_dqkv % vec || bp->ld_dout % vec) return DFK_EINVAL;
   const Geo g = make_geo(a);
+  if (a.dtype == DFK_BF16 && !a.mask && a.scale > 0.f && (a.tab || (!a.rpb && !g.use_mask))) {
+    // v3 (the forward's bias tiles, bwd layout)
+    const long units = (long)a.B * g.nW * a.heads;
+    if (units <= 0) return 0;
+    const bool tab = a.rpb || g.use_mask;
+    const bf16raw* tb = tab ? tab3_fwd(a, g) + tab_elems(a, g) : nullptr;
+    const int nkb = g.Np / 32;
+    const int nw = dfk_cdiv(nkb, dfk_cdiv(nkb, 8));   // passes of at most 8 waves, balanced
+    const size_t lds = bwd3_lds(a, g, nw);
+    if (lds > 160 * 1024) return DFK_EINVAL;
+    const bool want_drpb = a.rpb && bp->drpb;
+    if (want_drpb && !bp->ws) return DFK_EINVAL;
+    bf16raw* dsg = want_drpb ? reinterpret_cast<bf16raw*>(bp->ws) : nullptr;
+#define LAUNCH_B3(HD, TB, DR)                                                                              \
+  do {                                                                                                     \
+    auto kfn = wattn_bwd3_kernel<HD, TB, DR>;                                                              \
+    static bool attr_set = false;                                                                          \
+    if (!attr_set) {                                                                                       \
+      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+      attr_set = true;                                                                                     \
+    }                                                                                                      \
+    hipLaunchKernelGGL(kfn, dim3((unsigned)units), dim3(64 * nw), lds, s, *bp, g, dsg, tb);               \
+  } while (0)
+#define PICK_B3(HD)                                                                            \
+  do {                                                                                         \
+    if (tab) { if (a.drop.mode) LAUNCH_B3(HD, true, true); else LAUNCH_B3(HD, true, false); }  \
+    else { if (a.drop.mode) LAUNCH_B3(HD, false, true); else LAUNCH_B3(HD, false, false); }    \
+  } while (0)
+    if (a.hd == 32) PICK_B3(32); else PICK_B3(64);
+#undef PICK_B3
+#undef LAUNCH_B3
+    if (want_drpb) {
+      const DsPlan pl = ds_plan(a, g);
+      float* rows = reinterpret_cast<float*>(reinterpret_cast<char*>(bp->ws) + ((pl.ds_elems * 2 + 15) & ~15L));
+      hipLaunchKernelGGL(drpb_from_ds_kernel, dim3(pl.nchunks, a.heads, pl.nsplit), dim3(256),
+                         ((g.L + 3) & ~3) * 4, s, dsg, units, a.heads, g.Np, g.N, a.fh, a.fw, g.C0, g.L, pl.wps,
+                         rows);
+      hipLaunchKernelGGL(drpb_reduce_kernel, dim3(dfk_cdiv(g.L, 64), a.heads), dim3(1024), 0, s, rows, pl.rows,
+                         a.heads, g.L, bp->drpb);
+    }
+    DFK_CHECK_LAUNCH();
+    return 0;
+  }
   if (a.dtype == DFK_BF16) {
     const int nwaves = std::min(a.hd == 32 ? kBwdWaves : kBwdWaves / 2, g.Np / 32);  // hd 64: 4 waves, 512 VGPRs
     int Qn = g.Np;
@@ -2006,20 +2033,14 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
 #define LAUNCH_B16(HD, RPB, MASK)                                                                          \
   do {                                                                                                     \
     auto kfn = wattn_bwd_bf16_kernel<HD, RPB, MASK>;                                                       \
-    auto kft = a.drop.mode ? wattn_bwd_bf16_kernel<HD, RPB, false, true, true>                           \
-                           : wattn_bwd_bf16_kernel<HD, RPB, false, true, false>;                          \
     static bool attr_set = false;                                                                          \
     if (!attr_set) {                                                                                       \
       (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
-      (void)hipFuncSetAttribute((const void*)wattn_bwd_bf16_kernel<HD, RPB, false, true, false>,           \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                   \
-      (void)hipFuncSetAttribute((const void*)wattn_bwd_bf16_kernel<HD, RPB, false, true, true>,            \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                   \
       attr_set = true;                                                                                     \
     }                                                                                                      \
     for (int q0 = 0; q0 < g.Np; q0 += Qn)                                                                  \
-      hipLaunchKernelGGL(tabb ? kft : kfn, dim3((unsigned)units), dim3(64 * nwaves), lds, s, *bp, g, q0,   \
-                         std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0, dsg, tabb);                              \
+      hipLaunchKernelGGL(kfn, dim3((unsigned)units), dim3(64 * nwaves), lds, s, *bp, g, q0,                \
+                         std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0, dsg);                                    \
   } while (0)
 #define PICK_B16(HD)                                                 \
   do {                                                               \
@@ -2030,31 +2051,8 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     if (want_drpb && !bp->ws) return DFK_EINVAL;  // dRPB needs the dfk_wattn_bwd_workspace scratch
     const DsPlan pl = ds_plan(a, g);
     bf16raw* dsg = want_drpb ? reinterpret_cast<bf16raw*>(bp->ws) : nullptr;
-    // the forward left both table layouts in a.tab (same args, same rpb): the bwd layout follows the fwd one
-    const float* tabb = a.tab && !a.mask && a.scale > 0.f ? reinterpret_cast<const float*>(a.tab) + tab_elems(a, g)
-                                                          : nullptr;
-    if (a.drop.mode && !tabb) return DFK_EINVAL;   // attention dropout: table path only (as the forward)
-    static const int old_bwd = getenv("DFK_WATTN_BWD_OLD") ? atoi(getenv("DFK_WATTN_BWD_OLD")) : 0;
-    const size_t tlds = bwd_tab_lds(a, g, nwaves);
-    if (tabb && !old_bwd && tlds <= 160 * 1024) {
-#define LAUNCH_BT(HD, DR)                                                                              \
-  do {                                                                                                     \
-    auto kfn = wattn_bwd_tab_kernel<HD, DR>;                                                           \
-    static bool attr_set = false;                                                                          \
-    if (!attr_set) {                                                                                       \
-      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
-      attr_set = true;                                                                                     \
-    }                                                                                                      \
-    hipLaunchKernelGGL(kfn, dim3((unsigned)units), dim3(64 * nwaves), tlds, s, *bp, g, dsg, tabb);         \
-  } while (0)
-#define PICK_BT(HD)                                                                         \
-  do {                                                                                      \
-    if (a.drop.mode) LAUNCH_BT(HD, true); else LAUNCH_BT(HD, false);                        \
-  } while (0)
-      if (a.hd == 32) PICK_BT(32); else PICK_BT(64);
-#undef PICK_BT
-#undef LAUNCH_BT
-    } else if (a.hd == 32) PICK_B16(32); else PICK_B16(64);
+    if (a.drop.mode) return DFK_EINVAL;   // attention dropout: v3 kernels only (as the forward)
+    if (a.hd == 32) PICK_B16(32); else PICK_B16(64);
 #undef PICK_B16
 #undef LAUNCH_B16
     if (want_drpb) {
@@ -2099,7 +2097,8 @@ extern "C" int64_t dfk_wattn_table_workspace(const dfk_wattn_args* f) {
   if (!f || !args_ok(*f)) return -1;
   if (f->dtype != DFK_BF16 || f->mask) return 0;
   const Geo g = make_geo(*f);
-  return 4 * 2 * tab_elems(*f, g);   // fwd + bwd layouts, fp32
+  if (!f->rpb && !g.use_mask) return 0;   // no bias at all (wav2vec2): the kernels mask the padded keys themselves
+  return tab3_bytes(*f, g);   // bf16 fwd + bwd layouts
 }
 
 extern "C" int64_t dfk_wattn_bwd_workspace(const dfk_wattn_args* f) {

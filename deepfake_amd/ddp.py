@@ -28,23 +28,32 @@ import torch.distributed as dist
 
 
 def recorder_on():
-    """The ProcessGroupNCCL flight recorder is on (its size must be set before the process group exists)."""
-    return int(os.environ.get("TORCH_NCCL_TRACE_BUFFER_SIZE", "0") or 0) > 0
+    """The process-group flight recorder is on (its size must be set before the process group exists)."""
+    return max(int(os.environ.get(k, "0") or 0) for k in ("TORCH_FR_BUFFER_SIZE", "TORCH_NCCL_TRACE_BUFFER_SIZE")) > 0
 
 
 def watchdog_idle(timeout=60.0):
-    """Wait until the flight recorder lists no collective whose completion the ProcessGroupNCCL watchdog has not
-    yet discovered (onlyActive): then the watchdog queries no event.  Raises on timeout."""
+    """Wait until the flight recorder lists every collective as retired: the ProcessGroupNCCL watchdog marks a
+    work retired in the same critical section in which it drops the work from the list it polls, so after that
+    it queries none of their events again.  Raises on timeout."""
     import json
     import time
     from torch._C import _distributed_c10d as c10d
+    # the NCCL (RCCL) recorder and the generic one (gloo) are separate
+    dumps = [getattr(c10d, n) for n in ("_dump_nccl_trace_json", "_dump_fr_trace_json") if hasattr(c10d, n)]
     t0 = time.monotonic()
+    polls = 0
     while True:
-        d = json.loads(c10d._dump_nccl_trace_json(includeCollectives=True, onlyActive=True))
-        if not d.get("entries"):
+        ents = [e for dump in dumps for e in json.loads(dump(includeCollectives=True, onlyActive=False)).get("entries") or []]
+        live = [e for e in ents if not e.get("retired", False)]
+        polls += 1
+        if os.environ.get("DFK_DEBUG_WATCHDOG") and (polls == 1 or not live):
+            print(f"[watchdog_idle] poll {polls} t={time.monotonic() - t0:.4f}s entries={len(ents)} live={len(live)} "
+                  f"{[(e.get('profiling_name'), e.get('state')) for e in live[:4]]}", flush=True)
+        if not live:
             return
         if time.monotonic() - t0 > timeout:
-            raise RuntimeError(f"RCCL watchdog still tracks {len(d['entries'])} collectives after {timeout} s")
+            raise RuntimeError(f"RCCL watchdog still tracks {len(live)} collectives after {timeout} s")
         time.sleep(0.002)
 
 
@@ -156,9 +165,9 @@ class GradBucketer:
         """Deterministic drain before a HIP-graph capture.  The ProcessGroupNCCL watchdog thread queries the
         events of every eager collective until it has seen it complete, and HIP refuses that query once the
         RCCL stream has joined a capture (the watchdog then aborts the process).  So: wait for the given
-        works, idle the device, then poll the flight recorder (TORCH_NCCL_TRACE_BUFFER_SIZE > 0, set by
+        works, idle the device, then poll the flight recorder (TORCH_FR_BUFFER_SIZE > 0, set by
         bench.py / train.py before the process group exists) until the watchdog has retired every eager
-        collective of this process."""
+        collective of this process (watchdog_idle)."""
         for w in works:
             w.wait()
         if self.store.grad.is_cuda:

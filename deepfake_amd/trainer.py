@@ -158,7 +158,7 @@ class TrainStep:
             forms = tuple(f for f in forms if not f[0])
         if self.bucketer.enabled and not recorder_on():   # the same environment on every rank: all go eager
             forms = ()
-            err = RuntimeError("TORCH_NCCL_TRACE_BUFFER_SIZE unset: the RCCL watchdog cannot be observed idle")
+            err = RuntimeError("TORCH_FR_BUFFER_SIZE unset: the RCCL watchdog cannot be observed idle")
         for overlap, bn in forms:
             self.bucketer.drain(self.bucketer.last_works)
             g = torch.cuda.CUDAGraph()

@@ -66,7 +66,7 @@ def test_captured_overlapped_allreduce_single_rank():
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, DFK_DDP_FORCE="1", TORCH_NCCL_CUDA_EVENT_CACHE="0", TORCH_NCCL_TRACE_BUFFER_SIZE="256",
+    env = dict(os.environ, DFK_DDP_FORCE="1", TORCH_NCCL_CUDA_EVENT_CACHE="0", TORCH_FR_BUFFER_SIZE="256",
                MASTER_ADDR="127.0.0.1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
                         "--master-addr", "127.0.0.1", "--master-port", "29531",

@@ -86,7 +86,7 @@ def test_wattn_bwd(dt, case, table):
     scale = hd ** -0.5
     out, lse, tab = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, window, fw, shift, heads, hd, scale,
                                 rpb=rpb, pads=pads, use_table=table, return_table=True)
-    assert (tab is not None) == (table and dt == torch.bfloat16)
+    assert (tab is not None) == (table and dt == torch.bfloat16 and (rpb is not None or any(shift)))
     dout = torch.randn(rows, C, device=DEV, generator=g).to(dt)
     dqkv = torch.empty_like(qkv)
     drpb = torch.zeros(Lt, heads, device=DEV) if rpb is not None else None

@@ -11,7 +11,7 @@ import torch
 import torch.distributed as dist
 
 os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
-os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "256")
+os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "256")
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import synthetic_batch  # noqa: E402

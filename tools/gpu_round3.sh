@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU-box pass of round-3 evidence: parity tests, the default bench line (CPU baseline included), the
+# rocprofv3 kernel-trace stats of the same bench command, and the FETCH/WRITE PMC passes of the roofline kernel.
+# Each GPU step has its own time limit; the chain stops at the first failure.
+#   usage: bash tools/gpu_round3.sh TAG [skip-tests] [skip-cpu]
+set -o pipefail
+TAG=${1:-r3}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+if [ "$2" != "skip-tests" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
+  tail -3 $OUT/pytest_gpu.log
+fi
+CPU=""
+[ "$3" == "skip-cpu" ] && CPU="--no-cpu-baseline"
+timeout -k 10 500 python3 -u bench.py $CPU > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
+    python3 bench.py --no-cpu-baseline > $OUT/trace.log 2>&1 || { tail -30 $OUT/trace.log; exit 1; }
+python3 tools/prof_summary.py $(find $OUT/trace -name 'run_kernel_stats.csv' | head -1) 13 45 > $OUT/kernel_summary.txt
+head -30 $OUT/kernel_summary.txt
+timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_f -o run --output-format csv -- python3 tools/roofline_pmc.py run 5 > $OUT/pmc_f.log 2>&1 || { tail $OUT/pmc_f.log; exit 1; }
+timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_w -o run --output-format csv -- python3 tools/roofline_pmc.py run 5 > $OUT/pmc_w.log 2>&1 || { tail $OUT/pmc_w.log; exit 1; }
+python3 tools/roofline_pmc.py parse $(find $OUT/pmc_f -name run_counter_collection.csv) $(find $OUT/pmc_w -name run_counter_collection.csv) $OUT/${TAG}_wattn_fwd_pmc.json

@@ -49,7 +49,7 @@ def init_distributed():
     if world > 1 and not dist.is_initialized():
         # captured bucket all-reduces need RCCL work events outside torch's event cache (see bench.py)
         os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
-        os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "256")   # watchdog drain before capture (ddp.py)
+        os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "256")   # watchdog drain before capture (ddp.py)
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo",
                                 device_id=torch.device("cuda", local) if torch.cuda.is_available() else None)
     rank = dist.get_rank() if dist.is_initialized() else 0
