@@ -65,6 +65,12 @@ def build_parser():
     parser.add_argument('--val_clips', type=int, default=16)
     parser.add_argument('--test_clips', type=int, default=16)
     parser.add_argument('--frames', type=str, default='normalized', choices=['normalized', 'uint8'])
+    # f2 media front end on the device: mel slot input as the reference's cached image (fp32 normalised or the
+    # uint8 grey image) or as the raw 22.05 kHz waveform (device mel-spectrogram image); train-time frame
+    # augmentation (flips, rotation) of uint8 frames on the device
+    parser.add_argument('--mel_source', type=str, default='image', choices=['image', 'uint8', 'wave'])
+    parser.add_argument('--augment', action='store_true')
+    parser.add_argument('--bucket_dtype', type=str, default='fp32', choices=['fp32', 'bf16'])
     parser.add_argument('--bucket_mb', type=float, default=64.0)
     parser.add_argument('--deterministic', action='store_true')
     parser.add_argument('--video_encoder', type=str, default='swin', choices=['swin', 'inception'])

@@ -117,6 +117,11 @@ SIGNATURES = {
     "dfk_pool2d_bwd": [_VP, _I64, _VP, _I64, _VP, _I64, C.POINTER(Conv2dGeo), C.c_int, C.c_int, C.c_int, _VP],
     "dfk_dropout": [_VP, _VP, _I64, _I32, _I64, C.POINTER(Drop), C.c_int, _VP],
     "dfk_bernoulli_flags": [C.POINTER(Drop), _I32, _VP, _VP],
+    "dfk_mel_workspace": [_I64, _I64, _I32, _I32, _I32],
+    "dfk_mel_image": [_VP, _I64, _I64, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP],
+    "dfk_gray_normalize": [_VP, _VP, _I64, _I32, _I32, C.POINTER(C.c_float), C.POINTER(C.c_float), _VP],
+    "dfk_frame_augment": [_VP, _I64, _I32, _I32, _I32, _I32, _VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                          _VP, _VP],
     "dfk_layerdrop_flags": [C.POINTER(Drop), _I32, _VP, _VP, _VP],
     "dfk_spec_augment_fwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _F, _I32, _I32, C.POINTER(Drop), C.c_int, _VP],
     "dfk_spec_augment_bwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, C.c_int, _VP],
@@ -127,7 +132,7 @@ SIGNATURES = {
 }
 
 _lib = None
-RESTYPES = {"dfk_w2v_conv0_bwd_workspace": _I64, "dfk_layernorm_bwd_workspace": _I64, "dfk_wattn_bwd_workspace": _I64, "dfk_wattn_table_workspace": _I64, "dfk_gemm_workspace": _I64}
+RESTYPES = {"dfk_mel_workspace": _I64, "dfk_w2v_conv0_bwd_workspace": _I64, "dfk_layernorm_bwd_workspace": _I64, "dfk_wattn_bwd_workspace": _I64, "dfk_wattn_table_workspace": _I64, "dfk_gemm_workspace": _I64}
 
 
 def lib():

@@ -1913,8 +1913,22 @@ __global__ __launch_bounds__(256) void drpb_from_ds_kernel(const bf16raw* __rest
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const long nwin = units / heads;
     const long w0 = (long)split * wps, w1 = min(nwin, w0 + wps);
-    for (long w = w0; w < w1; ++w) {
-      const uint4 v = *reinterpret_cast<const uint4*>(ds + (w * heads + h) * NN + e0);
+    const bf16raw* src = ds + (w0 * heads + h) * NN + e0;
+    const long wstride = (long)heads * NN;
+    long w = w0;
+    for (; w + 8 <= w1; w += 8, src += 8 * wstride) {   // eight independent 16-B loads in flight per thread
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(src + u * wstride);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bf16raw* pe = reinterpret_cast<const bf16raw*>(&v[u]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f(pe[j]);
+      }
+    }
+    for (; w < w1; ++w, src += wstride) {
+      const uint4 v = *reinterpret_cast<const uint4*>(src);
       const bf16raw* pe = reinterpret_cast<const bf16raw*>(&v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += bf2f(pe[j]);
@@ -1945,7 +1959,9 @@ DsPlan ds_plan(const dfk_wattn_args& a, const Geo& g) {
   pl.ds_elems = units * g.Np * g.Np;
   pl.nchunks = (int)dfk_cdiv((long)g.Np * g.Np, 256 * 8);
   const long nwin = units / a.heads;
-  pl.wps = 64;
+  // about 1.5k workgroups over the chip, each summing wps windows (fewer, longer sums: fewer partial rows)
+  const long want = std::max<long>(1, std::min<long>(nwin, 1536 / std::max(1, pl.nchunks * a.heads)));
+  pl.wps = (int)dfk_cdiv(nwin, want);
   pl.nsplit = (int)dfk_cdiv(nwin, pl.wps);
   pl.rows = (long)pl.nsplit * pl.nchunks * a.heads;
   return pl;

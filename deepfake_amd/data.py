@@ -4,7 +4,10 @@ seeded stream instead of decoded from mp4 files (no media ships with the repo; t
 is defined on synthetic clips).
 
 Items follow DeepFake.__getitem__ (:135-173) with modality 'fused':
-  ({"Video": frames, "Audio": mel image [3,224,224], "PAudio": waveform (np.float32, raw)}, label, name)
+  ({"Video": frames, "Audio": mel input, "PAudio": waveform (np.float32, raw)}, label, name)
+  mel input: 'image' -> [3,224,224] fp32 (the normalised cached JPEG), 'uint8' -> [224,224] grey image (the
+             trainer normalises it on the GPU), 'wave' -> 22.05 kHz waveform (the GPU builds the mel image,
+             deepfake_amd.media, then normalises it)
   frames: 'normalized' -> [T,3,H,W] fp32, what extract_frames + T.Normalize produce (:55-69, utils.py:22-39)
           'uint8'      -> [T,H,W,3] uint8 decoded RGB frames; the trainer normalises them on the GPU
                           (deepfake_amd.kernels.frame_normalize: ToTensor + Normalize fused)
@@ -26,9 +29,11 @@ def _rng(seed, index):
 class DeepFake(Dataset):
     """Synthetic clips: label ~ Bernoulli(0.5); frames, mel image and waveform from the seeded stream."""
 
-    def __init__(self, args, split="train", n=64, seed=0, frames="normalized", T=None, H=224, W=224, seconds=4):
+    def __init__(self, args, split="train", n=64, seed=0, frames="normalized", T=None, H=224, W=224, seconds=4,
+                 mel_source="image"):
         self.args, self.split, self.n, self.seed = args, split, int(n), int(seed) + {"train": 0, "val": 1, "test": 2}[split]
         self.frames = frames
+        self.mel_source = mel_source
         self.T = T or getattr(args, "num_frames", 32)
         self.H, self.W, self.seconds = H, W, seconds
         self.modality = getattr(args, "modality", "fused")
@@ -51,7 +56,12 @@ class DeepFake(Dataset):
         name = f"synthetic_{self.split}_{index:06d}.mp4"
         label = torch.tensor(float(g.uniform() < 0.5), dtype=torch.float32)
         video = self._video(g)
-        mel = torch.from_numpy(g.standard_normal((3, 224, 224), dtype=np.float32))
+        if self.mel_source == "uint8":       # the cached grey JPEG as decoded (data_process.py:83-93,162)
+            mel = torch.from_numpy(g.integers(0, 256, size=(224, 224), dtype=np.uint8))
+        elif self.mel_source == "wave":      # the waveform librosa.load hands generate_mel_spectrogram (22.05 kHz)
+            mel = torch.from_numpy((0.1 * g.standard_normal(int(22050 * self.seconds))).astype(np.float32))
+        else:
+            mel = torch.from_numpy(g.standard_normal((3, 224, 224), dtype=np.float32))
         wave = (0.1 * g.standard_normal(int(16000 * self.seconds))).astype(np.float32)
         feat = {"video": video, "audio": mel, "paudio": wave.copy()}.get(self.modality)
         if self.modality == "fused":
@@ -96,7 +106,8 @@ class DeepFakeSet:
         self.trainset = self.valset = self.testset = None
 
     def setup(self, event=None, stage=None):
-        a, kw = self.args, dict(frames=getattr(self.args, "frames", "normalized"), **self.clip_shape)
+        a, kw = self.args, dict(frames=getattr(self.args, "frames", "normalized"),
+                                mel_source=getattr(self.args, "mel_source", "image"), **self.clip_shape)
         seed = getattr(a, "random_seed", 0) * 7919 + (self.rank or 0)      # distinct clips per rank
         self.trainset = DeepFake(a, "train", getattr(a, "train_clips", 64), seed, **kw)
         self.valset = DeepFake(a, "val", getattr(a, "val_clips", 16), seed, **kw)

@@ -48,12 +48,34 @@ def normalize_wave(w):
     return K.wave_normalize(w)
 
 
-def prepare_video(video, device):
-    """Frames to the device: fp32 transform output as is; decoded uint8 RGB frames [B,T,H,W,3] normalised on
-    the GPU (T.ToTensor + T.Normalize, data/data_process.py:55-69) -> [B,T,3,H,W]."""
+def prepare_video(video, device, augment=False, generator=None):
+    """Frames to the device: fp32 transform output as is; decoded uint8 RGB frames [B,T,H,W,3] transformed on
+    the GPU -> [B,T,3,H,W]: T.ToTensor + T.Normalize (data/data_process.py:55-60, eval), or with augment the
+    training transform (:62-69: Resize, RandomHorizontalFlip, RandomVerticalFlip, RandomRotation(90), drawn per
+    frame as the reference transforms every frame separately)."""
     from . import kernels as K
+    from . import media
     v = video.to(device, non_blocking=True)
-    return K.frame_normalize(v) if v.dtype == torch.uint8 else v
+    if v.dtype != torch.uint8:
+        return v
+    if not augment:
+        return K.frame_normalize(v)
+    n = v.numel() // (v.shape[-3] * v.shape[-2] * 3)
+    flips, angles = media.draw_augment(n, v.device, generator)
+    return media.frame_augment(v, flips=flips, angles=angles)
+
+
+def prepare_mel(audio, device):
+    """The mel slot's input to the device: the normalised image as is; the uint8 grey image (the reference's
+    cached JPEG, data_process.py:162) normalised on the GPU; a raw 22.05 kHz waveform [B, S] turned into the
+    mel-spectrogram image on the GPU first (generate_mel_spectrogram, src/utils.py:63-87)."""
+    from . import media
+    a = audio.to(device, non_blocking=True)
+    if a.dtype == torch.uint8:
+        return media.gray_normalize(a)
+    if a.dim() == 2:
+        return media.gray_normalize(media.mel_image(a))
+    return a
 
 
 class TrainStep:
@@ -216,6 +238,7 @@ class Trainer:
         self.log_step = args.log_step
         self.start_epoch = 0
         self.accum_step = max(1, int(args.accum_step))
+        self.augment = bool(getattr(args, "augment", False))
         self.dataset = dataset
         self.trainloader = dataset.train_dataloader()
         self.valloader = dataset.val_dataloader()
@@ -227,7 +250,9 @@ class Trainer:
         model.to(device)
         self.model_s = self.model = model
         self.store = ParamStore(model, dt)
-        self.bucketer = GradBucketer(self.store, bucket_mb=getattr(args, "bucket_mb", 64.0))
+        self.bucketer = GradBucketer(self.store, bucket_mb=getattr(args, "bucket_mb", 64.0),
+                                     comm_dtype=torch.bfloat16 if getattr(args, "bucket_dtype", "fp32") == "bf16"
+                                     else torch.float32)
         self.bucketer.broadcast_buffers(model)
         if self.bucketer.enabled:                      # identical replicas: parameters from rank 0
             dist.broadcast(self.store.flat, 0)
@@ -261,14 +286,15 @@ class Trainer:
     def _features(self, feat):
         """src/trainer.py:250-262: the batch's features on the device, waveforms padded to the longest and
         normalised (the processor), frames normalised when they arrive as decoded uint8."""
+        aug = self.augment and self.model.training
         if self.modality == "fused":
             wave = normalize_wave(pad_longest(feat["PAudio"]).to(self.device, non_blocking=True))
-            return (prepare_video(feat["Video"], self.device), feat["Audio"].to(self.device, non_blocking=True), wave)
+            return (prepare_video(feat["Video"], self.device, aug), prepare_mel(feat["Audio"], self.device), wave)
         if self.modality == "paudio":
             return normalize_wave(pad_longest(feat).to(self.device, non_blocking=True))
         if self.modality == "video":
-            return prepare_video(feat, self.device)
-        return feat.to(self.device, non_blocking=True)
+            return prepare_video(feat, self.device, aug)
+        return prepare_mel(feat, self.device)
 
     def _prep(self, batch):
         return self._features(batch[0]), batch[1].to(self.device, non_blocking=True)

@@ -332,6 +332,31 @@ int dfk_frame_normalize(const uint8_t* src, float* dst, int64_t frames, int32_t 
  * zero-padded [B, S] batch (no attention mask, Q13): y = (x - mean) / sqrt(var + eps), eps = 1e-7. */
 int dfk_wave_normalize(const float* x, float* y, int64_t B, int64_t S, float eps, hipStream_t stream);
 
+/* ---- media front end on the device (csrc/media.hip) ----
+ * Mel-spectrogram image of generate_mel_spectrogram (src/utils.py:63-87): librosa.feature.melspectrogram(y, sr,
+ * n_mels) with its defaults (periodic Hann window of n_fft, hop, center=True zero padding, power 2) ->
+ * power_to_db(ref=max, amin 1e-10, top_db 80) -> cv2.normalize(NORM_MINMAX, 0, 255) -> uint8 (truncation) ->
+ * cv2.resize(out_w x out_h, INTER_LINEAR, uint8 fixed point).  wave fp32 [B, S] at the filterbank's sample rate
+ * (S % 4 == 0 for the vector path); basis fp32 [n_fft][ld] with ld = 2*(n_fft/2+1) rounded up to 4: the
+ * window-folded cos | -sin DFT basis; fbank fp32 [n_mels][n_fft/2+1] (Slaney); ws of dfk_mel_workspace bytes;
+ * out uint8 [B, out_h, out_w].  The STFT runs on dfk_gemm (fp32 MFMA). */
+int64_t dfk_mel_workspace(int64_t B, int64_t S, int32_t n_fft, int32_t hop, int32_t n_mels);
+int dfk_mel_image(const float* wave, int64_t B, int64_t S, const float* basis, const float* fbank, int32_t n_fft,
+                  int32_t hop, int32_t n_mels, int32_t out_h, int32_t out_w, void* ws, int64_t ws_bytes, uint8_t* out,
+                  hipStream_t stream);
+/* Gray uint8 [n, H, W] -> fp32 [n, 3, H, W]: Image.convert('RGB') + T.ToTensor() + T.Normalize(mean, std)
+ * (data_process.py:55-69,162); mean3 / std3 are HOST arrays of 3 floats. */
+int dfk_gray_normalize(const uint8_t* src, float* dst, int64_t n_img, int32_t H, int32_t W, const float* mean3,
+                       const float* std3, hipStream_t stream);
+/* Train-time frame transform of data_process.py:62-69 fused per output pixel: T.Resize((out_h, out_w)) (bilinear,
+ * half-pixel centres, rounded to uint8), T.RandomHorizontalFlip (flips[f] bit 0), T.RandomVerticalFlip (bit 1),
+ * T.RandomRotation (angles[f] degrees; torchvision F.rotate on tensors: nearest, fill 0, no expand),
+ * T.ToTensor + T.Normalize.  src uint8 [frames, H, W, 3] (decoded RGB), dst fp32 [frames, 3, out_h, out_w];
+ * flips / angles are DEVICE arrays of one entry per frame (NULL: no flip / no rotation); mean3 / std3 HOST. */
+int dfk_frame_augment(const uint8_t* src, int64_t frames, int32_t H, int32_t W, int32_t out_h, int32_t out_w,
+                      const int32_t* flips, const float* angles, const float* mean3, const float* std3, float* dst,
+                      hipStream_t stream);
+
 /* ---- 2-D convolution family of the Inception-ResNet-v2 video branch (SURVEY.md §8f f4:
  * src/models/InceptionResV2.py:6-190, IResNet.py:331-393).  Activations are channels-last [N*H*W, C] rows with
  * a row stride ld (>= C), so a branch reads / writes a channel slice of a torch.cat buffer in place. */

@@ -56,3 +56,15 @@ def test_product_has_no_cpu_fallback():
     from deepfake_amd import _lib
     with pytest.raises(RuntimeError):
         _lib.ptr(torch.zeros(4))
+
+
+def test_header_parameter_counts_match_binding():
+    """Every prototype of include/dfk.h has as many parameters as its ctypes argtypes entry (a changed C
+    signature — e.g. dfk_w2v_conv0_bwd's scratch_bytes — cannot drift from the binding)."""
+    from deepfake_amd import _lib
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    protos = re.findall(r"^(?:int|int64_t)\s+(dfk_\w+)\s*\(([^;]*)\)\s*;", src, flags=re.M | re.S)
+    assert protos
+    for name, params in protos:
+        n = 0 if params.strip() in ("", "void") else params.count(",") + 1
+        assert n == len(_lib.SIGNATURES[name]), (name, n, len(_lib.SIGNATURES[name]))

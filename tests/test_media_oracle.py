@@ -1,0 +1,55 @@
+"""CPU: the f2 media oracle (oracle/media.py) — STFT power against torch.stft, the Slaney filterbank's
+defining properties, the cv2 fixed-point resize on exact cases, and the product's host-side constants
+(deepfake_amd.media: DFT basis, filterbank) against the oracle's restatement.  librosa / cv2 are absent:
+parity unpinned against them."""
+import numpy as np
+import torch
+
+from oracle import media as OM
+
+
+def test_stft_power_matches_torch_stft():
+    g = np.random.default_rng(0)
+    y = g.standard_normal(22050).astype(np.float32)
+    p = OM.stft_power(y, 2048, 512)
+    X = torch.stft(torch.from_numpy(y).double(), n_fft=2048, hop_length=512,
+                   window=torch.hann_window(2048, periodic=True, dtype=torch.float64), center=True,
+                   pad_mode="constant", return_complex=True)
+    ref = (X.abs() ** 2).numpy()
+    assert p.shape == ref.shape == (1025, 1 + 22050 // 512)
+    assert np.abs(p - ref).max() <= 1e-9 * ref.max()
+
+
+def test_slaney_filterbank_properties():
+    fb = OM.mel_filters(22050, 2048, 128).astype(np.float64)
+    assert fb.shape == (128, 1025) and (fb >= 0).all()
+    freqs = np.linspace(0, 11025, 1025)
+    # Slaney area normalisation: each triangle integrates (over Hz) to ~1 (up to the bin sampling)
+    area = (fb * (freqs[1] - freqs[0])).sum(1)
+    assert np.allclose(area[8:], 1.0, rtol=0.08)
+    # band centres increase with the mel index; below 1 kHz the scale is linear (200/3 Hz per mel)
+    peaks = freqs[fb.argmax(1)]
+    assert (np.diff(peaks) >= 0).all()
+    assert abs(OM.hz_to_mel(np.array([1000.0]))[0] - 15.0) < 1e-12
+    assert abs(OM.mel_to_hz(OM.hz_to_mel(np.array([4321.0])))[0] - 4321.0) < 1e-9
+
+
+def test_cv_resize_identity_and_constant():
+    g = np.random.default_rng(1)
+    img = g.integers(0, 256, size=(37, 53), dtype=np.uint8)
+    assert np.array_equal(OM.cv_resize_linear_u8(img, (53, 37)), img)
+    c = np.full((20, 30), 77, dtype=np.uint8)
+    assert (OM.cv_resize_linear_u8(c, (224, 224)) == 77).all()
+
+
+def test_product_constants_match_oracle():
+    from deepfake_amd import media
+    fb = media.mel_filterbank(22050, 2048, 128)
+    assert np.allclose(fb, OM.mel_filters(22050, 2048, 128), rtol=1e-6, atol=1e-9)
+    b = media.stft_basis(2048).astype(np.float64)
+    g = np.random.default_rng(2)
+    fr = g.standard_normal(2048)
+    X = np.fft.rfft(fr * (0.5 - 0.5 * np.cos(2 * np.pi * np.arange(2048) / 2048)))
+    got = fr @ b
+    assert np.abs(got[:1025] - X.real).max() < 1e-4 and np.abs(got[1025:2050] - X.imag).max() < 1e-4
+    assert b.shape == (2048, 2052) and not b[:, 2050:].any()
