@@ -587,9 +587,11 @@ __device__ __forceinline__ int win_class(const dfk_wattn_args& a, const Geo& g, 
          (a.sw > 0 && wwi == g.nww - 1 ? 1 : 0);
 }
 
-// Work order of the table kernels: units sorted by (shift class, head, clip, window) and dealt to the
-// XCDs in contiguous chunks (blocks b and b+8 share an XCD), so the workgroups that read one (class,
-// head) table run together on one XCD and the table is read from that XCD's L2.
+// Work order of the table kernels: units sorted by (shift class, clip, window, head) and dealt to the
+// XCDs in contiguous chunks (blocks b and b+8 share an XCD).  The heads of one window run back to back on
+// one XCD: head h's q / k / v columns are 2 HD bytes of a 6 C-byte token row, so one head alone uses part
+// of every 128-B line it fetches, and its siblings take the rest from that XCD's L2 instead of fetching
+// the line again from HBM.  A class's tables (heads x Np^2 bf16, ~1 MB at stage 1) stay L2-resident too.
 struct WUnit {
   int b, win, head, cls, qpart;
   long lse_unit;   // (b*nW + win)*heads + head: the lse row, as the table-free kernels index it
@@ -613,8 +615,8 @@ __device__ __forceinline__ WUnit decode_unit(const dfk_wattn_args& a, const Geo&
     u -= cnt;
   }
   const int perw = nd * nh * nw;
-  w.head = u / (perw * a.B);
-  u %= perw * a.B;
+  w.head = u % a.heads;
+  u /= a.heads;
   w.b = u / perw;
   u %= perw;
   const int id = u / (nh * nw), ih = (u / nw) % nh, iw = u % nw;
@@ -1647,44 +1649,45 @@ constexpr int kSdRow = 32;   // bf16 per row of the [32 keys][32 queries] dS^T s
 __device__ __forceinline__ int sd_off(int k, int q) { return k * kSdRow + ((((q >> 2) ^ (k >> 1)) & 7) << 2) + (q & 3); }
 
 template <int HD, bool TAB, bool DROP>
-__global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_args ba, const Geo g,
-                                                         bf16raw* __restrict__ dsg, const bf16raw* __restrict__ tabb) {
+__global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_args ba, const Geo g, int q0, int Qn,
+                                                         int accum_kv, bf16raw* __restrict__ dsg,
+                                                         const bf16raw* __restrict__ tabb) {
   constexpr int NKK = HD / 16, NOT = HD / 32, CH = HD / 8;
   const dfk_wattn_args& a = ba.f;
   const int nw = blockDim.x >> 6;
-  const int Np = g.Np, nkb = Np / 32, nqb = Np / 32;
+  // queries [q0, q0 + Qn) of every window (Qn = Np unless the window's Q / dO / dQ do not fit the LDS: then
+  // several launches, dK / dV accumulated in place by the later ones)
+  const int Np = g.Np, nkb = Np / 32, nqb = Qn / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* p = smem;
-  float* dQa = reinterpret_cast<float*>(p); p += 4 * (size_t)Np * HD;   // [qb][ot][v][lane][4]
-  bf16raw* Qs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;  // Q' = Q scale log2e
-  bf16raw* dOs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;
+  float* dQa = reinterpret_cast<float*>(p); p += 4 * (size_t)Qn * HD;   // [qb][ot][v][lane][4]
+  bf16raw* Qs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Qn * HD;  // Q' = Q scale log2e
+  bf16raw* dOs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Qn * HD;
   bf16raw* Sd = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)nw * 32 * kSdRow;
   int* trow = reinterpret_cast<int*>(p); p += 4 * Np;
-  float* nl2 = reinterpret_cast<float*>(p); p += 4 * Np;   // -lse log2e; -inf beyond N (P = 0)
-  float* ndl = reinterpret_cast<float*>(p); p += 4 * Np;   // -delta
+  float* nl2 = reinterpret_cast<float*>(p); p += 4 * Qn;   // -lse log2e; -inf beyond N (P = 0)
+  float* ndl = reinterpret_cast<float*>(p); p += 4 * Qn;   // -delta
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
-  int unit = blockIdx.x;
-  const int head = unit % a.heads;
-  unit /= a.heads;
-  const int win = unit % g.nW, b = unit / g.nW;
+  const WUnit wu = decode_unit(a, g, 1);   // the forward's work order; lse / dS^T / dropout rows by lse_unit
+  const int head = wu.head, win = wu.win, b = wu.b;
+  const long unit = wu.lse_unit;
   const int hoff = head * HD;
-  const bf16raw* tch = TAB ? tabb + ((long)win_class(a, g, win) * a.heads + head) * (long)Np * Np + lane * 8 : nullptr;
+  const bf16raw* tch = TAB ? tabb + ((long)wu.cls * a.heads + head) * (long)Np * Np + lane * 8 : nullptr;
   const float qs = a.scale * kLog2e;
 
-  for (int i = tid; i < Np; i += blockDim.x) {
-    trow[i] = token_info_row(a, g, b, win, i);
-    nl2[i] = i < g.N ? -a.lse[(long)blockIdx.x * Np + i] * kLog2e : -INFINITY;
-  }
-  for (int i = tid * 4; i < Np * HD; i += blockDim.x * 4) *reinterpret_cast<f32x4*>(dQa + i) = f32x4{0, 0, 0, 0};
+  for (int i = tid; i < Np; i += blockDim.x) trow[i] = token_info_row(a, g, b, win, i);
+  for (int i = tid; i < Qn; i += blockDim.x)
+    nl2[i] = q0 + i < g.N ? -a.lse[unit * Np + q0 + i] * kLog2e : -INFINITY;
+  for (int i = tid * 4; i < Qn * HD; i += blockDim.x * 4) *reinterpret_cast<f32x4*>(dQa + i) = f32x4{0, 0, 0, 0};
   __syncthreads();
-  for (int base = 0; base < Np * CH; base += blockDim.x) {
+  for (int base = 0; base < Qn * CH; base += blockDim.x) {
     const int idx = base + tid;
     float d = 0.f;
-    if (idx < Np * CH) {
+    if (idx < Qn * CH) {
       const int li = idx / CH, c = (idx % CH) * 8;
-      const int row = trow[li];
+      const int row = trow[q0 + li];
       uint4 qv = tok_ld16<bf16raw>(a.q, a.pad_q, row, a.ld_qkv, hoff + c);
       const uint4 dv = tok_ld16<bf16raw>(ba.dout, nullptr, row, ba.ld_dout, hoff + c);
       const uint4 ov = tok_ld16<bf16raw>(a.out, nullptr, row, a.ld_out, hoff + c);
@@ -1697,7 +1700,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
     }
 #pragma unroll
     for (int o = 1; o < CH; o <<= 1) d += __shfl_xor(d, o, 64);
-    if (idx < Np * CH && (idx % CH) == 0) ndl[idx / CH] = -d;
+    if (idx < Qn * CH && (idx % CH) == 0) ndl[idx / CH] = -d;
   }
   __syncthreads();
 
@@ -1705,7 +1708,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   bias_ident(lane, id0, id1, sel);
   bf16raw* Sw = Sd + wave * 32 * kSdRow;
   const DropCtx dc = drop_ctx(a.drop);
-  bf16raw* dsu = dsg ? dsg + (long)blockIdx.x * Np * Np : nullptr;   // this window-head's dS^T [k][q]
+  bf16raw* dsu = dsg ? dsg + unit * Np * Np : nullptr;   // this window-head's dS^T [k][q]
   for (int pass = 0; pass * nw < nkb; ++pass) {
     const int kb = pass * nw + wave;
     if (kb >= nkb) {   // no key block this pass: keep the step barriers
@@ -1740,19 +1743,19 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
       if constexpr (TAB) {
 #pragma unroll
         for (int c = 0; c < 2; ++c)
-          bt[c] = *reinterpret_cast<const bf16x8*>(tch + ((long)(qb * nkb + kb) * 2 + c) * 512);
+          bt[c] = *reinterpret_cast<const bf16x8*>(tch + ((long)((q0 / 32 + qb) * nkb + kb) * 2 + c) * 512);
       }
     };
     int qb = wave % nqb;
     load_bias(qb);
     for (int i = 0; i < nqb; ++i, qb = qb + 1 == nqb ? 0 : qb + 1) {
-      const int q0 = qb * 32;
+      const int qr0 = qb * 32;   // local row of the block in the chunk
       // row constants as the C inputs: queries q0 + 8 v + 4 hh + (0..3) in registers 4v .. 4v+3
       f32x16 s, dp;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(nl2 + q0 + 8 * v + 4 * hh);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(ndl + q0 + 8 * v + 4 * hh);
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(nl2 + qr0 + 8 * v + 4 * hh);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(ndl + qr0 + 8 * v + 4 * hh);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           s[4 * v + t] = l4[t] + kneg;
@@ -1761,7 +1764,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
       }
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
-        const int off = swz<HD>(q0 + r, kk * 16 + hh * 8);
+        const int off = swz<HD>(qr0 + r, kk * 16 + hh * 8);
         const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + off);
         const bf16x8 da = *reinterpret_cast<const bf16x8*>(dOs + off);
         s = mfma32(qa, kB[kk], s);
@@ -1780,8 +1783,8 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
         for (int j = 0; j < 8; ++j) {
           const float P = __builtin_amdgcn_exp2f(s[8 * c + j]);
           if constexpr (DROP) {
-            const int q = q0 + 8 * (2 * c + (j >> 2)) + 4 * hh + (j & 3);
-            const float mk = drop_mul(dc, (long)blockIdx.x * Np + q, kb * 32 + r);
+            const int q = qr0 + 8 * (2 * c + (j >> 2)) + 4 * hh + (j & 3);
+            const float mk = drop_mul(dc, unit * Np + q0 + q, kb * 32 + r);
             pa[c][j] = (__bf16)(P * mk);
             sa[c][j] = (__bf16)(P * (dp[8 * c + j] * mk + ndl[q]));
           } else {
@@ -1799,7 +1802,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
       // dV^T += dO^T P, dK^T += Q'^T dS: A rows e = 32 ot + r, k-step c slots <-> queries 16 c + 8 (j>>2) + 4 hh + (j&3)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const int qr = q0 + 16 * c + 4 * (g16 >> 1) + tq;
+        const int qr = qr0 + 16 * c + 4 * (g16 >> 1) + tq;
 #pragma unroll
         for (int ot = 0; ot < NOT; ++ot) {
           const int col = ot * 32 + 16 * (g16 & 1) + 4 * tp;
@@ -1830,7 +1833,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
         const uint2 x1 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 4));
         const uint2 x2 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 8));
         const uint2 x3 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 12));
-        bf16raw* gp = dsu + (long)(kb * 32 + kr) * Np + q0 + half * 16;
+        bf16raw* gp = dsu + (long)(kb * 32 + kr) * Np + q0 + qr0 + half * 16;
         *reinterpret_cast<uint4*>(gp) = make_uint4(x0.x, x0.y, x1.x, x1.y);
         *reinterpret_cast<uint4*>(gp + 8) = make_uint4(x2.x, x2.y, x3.x, x3.y);
       }
@@ -1853,13 +1856,22 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
       for (int v = 0; v < 4; ++v) {
         const int e = hoff + ot * 32 + 8 * v + 4 * hh;
         if (krow >= 0) {
+          bf16raw* pk = reinterpret_cast<bf16raw*>(ba.dk) + (long)krow * ba.ld_dqkv + e;
+          bf16raw* pv = reinterpret_cast<bf16raw*>(ba.dv) + (long)krow * ba.ld_dqkv + e;
+          float vk[4], vv[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) { vk[t] = dKt[ot][4 * v + t] * kscale; vv[t] = dVt[ot][4 * v + t]; }
+          if (accum_kv) {   // a later query chunk: add to the earlier chunks' partial sums
+#pragma unroll
+            for (int t = 0; t < 4; ++t) { vk[t] += bf2f(pk[t]); vv[t] += bf2f(pv[t]); }
+          }
           uint2 uk, uv;
-          uk.x = (uint32_t)f2bf(dKt[ot][4 * v] * kscale) | ((uint32_t)f2bf(dKt[ot][4 * v + 1] * kscale) << 16);
-          uk.y = (uint32_t)f2bf(dKt[ot][4 * v + 2] * kscale) | ((uint32_t)f2bf(dKt[ot][4 * v + 3] * kscale) << 16);
-          uv.x = (uint32_t)f2bf(dVt[ot][4 * v]) | ((uint32_t)f2bf(dVt[ot][4 * v + 1]) << 16);
-          uv.y = (uint32_t)f2bf(dVt[ot][4 * v + 2]) | ((uint32_t)f2bf(dVt[ot][4 * v + 3]) << 16);
-          *reinterpret_cast<uint2*>(reinterpret_cast<bf16raw*>(ba.dk) + (long)krow * ba.ld_dqkv + e) = uk;
-          *reinterpret_cast<uint2*>(reinterpret_cast<bf16raw*>(ba.dv) + (long)krow * ba.ld_dqkv + e) = uv;
+          uk.x = (uint32_t)f2bf(vk[0]) | ((uint32_t)f2bf(vk[1]) << 16);
+          uk.y = (uint32_t)f2bf(vk[2]) | ((uint32_t)f2bf(vk[3]) << 16);
+          uv.x = (uint32_t)f2bf(vv[0]) | ((uint32_t)f2bf(vv[1]) << 16);
+          uv.y = (uint32_t)f2bf(vv[2]) | ((uint32_t)f2bf(vv[3]) << 16);
+          *reinterpret_cast<uint2*>(pk) = uk;
+          *reinterpret_cast<uint2*>(pv) = uv;
         } else if (krow == -1) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
@@ -1871,9 +1883,9 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   }
   __syncthreads();
   // dQ rows (scaled): (q, e) of block qb sits at [qb][ot][v][lane][t], q = 32 qb + 8 v + 4 h + t, lane = (e & 31) + 32 h
-  for (int t8 = tid; t8 < Np * (HD / 8); t8 += blockDim.x) {
+  for (int t8 = tid; t8 < Qn * (HD / 8); t8 += blockDim.x) {
     const int i = t8 / (HD / 8), c = (t8 % (HD / 8)) * 8;
-    const int row = i < g.N ? trow[i] : -2;
+    const int row = q0 + i < g.N ? trow[q0 + i] : -2;
     const int qb = i >> 5, qi = i & 31, v = qi >> 3, h2 = (qi >> 2) & 1, t = qi & 3, ot = c >> 5;
     const float* src = dQa + ((size_t)((qb * NOT + ot) * 4 + v) * 64 + (c & 31) + 32 * h2) * 4 + t;
     float vv[8];
@@ -1892,8 +1904,8 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   }
 }
 
-size_t bwd3_lds(const dfk_wattn_args& a, const Geo& g, int nw) {
-  return 8 * (size_t)g.Np * a.hd + 2 * (size_t)nw * 32 * kSdRow + 12 * (size_t)g.Np;
+size_t bwd3_lds(const dfk_wattn_args& a, const Geo& g, int Qn, int nw) {
+  return 8 * (size_t)Qn * a.hd + 2 * (size_t)nw * 32 * kSdRow + 4 * (size_t)g.Np + 8 * (size_t)Qn;
 }
 
 // dRPB from the dS^T scratch: drpb[pos(q) - pos(k) + C0] += sum over windows of dS[q][k].
@@ -2002,8 +2014,13 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     const bool tab = a.rpb || g.use_mask;
     const bf16raw* tb = tab ? tab3_fwd(a, g) + tab_elems(a, g) : nullptr;
     const int nkb = g.Np / 32;
-    const int nw = dfk_cdiv(nkb, dfk_cdiv(nkb, 8));   // passes of at most 8 waves, balanced
-    const size_t lds = bwd3_lds(a, g, nw);
+    int nw = dfk_cdiv(nkb, dfk_cdiv(nkb, 8));   // passes of at most 8 waves, balanced
+    int Qn = g.Np;                               // largest query chunk whose Q / dO / dQ fit the LDS ...
+    while (Qn > 32 && bwd3_lds(a, g, Qn, nw) > 160 * 1024) Qn -= 32;
+    const int nch = dfk_cdiv(g.Np, Qn);          // ... then balanced chunks
+    Qn = 32 * dfk_cdiv(g.Np / 32, nch);
+    nw = std::min(nw, g.Np / 32 - (nch - 1) * (Qn / 32));   // the staggered sweep needs a distinct block per wave
+    const size_t lds = bwd3_lds(a, g, Qn, nw);
     if (lds > 160 * 1024) return DFK_EINVAL;
     const bool want_drpb = a.rpb && bp->drpb;
     if (want_drpb && !bp->ws) return DFK_EINVAL;
@@ -2016,7 +2033,9 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
       (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
       attr_set = true;                                                                                     \
     }                                                                                                      \
-    hipLaunchKernelGGL(kfn, dim3((unsigned)units), dim3(64 * nw), lds, s, *bp, g, dsg, tb);               \
+    for (int q0 = 0; q0 < g.Np; q0 += Qn)                                                                  \
+      hipLaunchKernelGGL(kfn, dim3((unsigned)units), dim3(64 * nw), lds, s, *bp, g, q0,                    \
+                         std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0, dsg, tb);                                \
   } while (0)
 #define PICK_B3(HD)                                                                            \
   do {                                                                                         \

@@ -101,6 +101,7 @@ class TrainStep:
         self.static = None
         self.captured_overlap = None     # form of the captured step (None: not captured)
         self.captured_bn = False
+        self.agraphs = None              # accumulation: (non-final micro-step, final micro-step) graphs
         self.first_micro = True
         if not bucketer.bn_buffers:
             bucketer.track_batchnorm(model)
@@ -115,6 +116,12 @@ class TrainStep:
         return loss, prob
 
     def micro(self, feature, label, last, accum=1):
+        """One micro-step of an accumulation window (eager, or replayed from the window's two graphs)."""
+        if self.graph_mode and accum > 1:
+            return self._micro_graphed(feature, label, last, accum)
+        return self._micro_eager(feature, label, last, accum)
+
+    def _micro_eager(self, feature, label, last, accum):
         if self.first_micro:
             self.bucketer.broadcast_bn()
             self.first_micro = False
@@ -131,20 +138,45 @@ class TrainStep:
         return loss.detach(), prob.detach()
 
     def eager(self, feature, label):
-        return self.micro(feature, label, True, 1)
+        return self._micro_eager(feature, label, True, 1)
 
     def __call__(self, feature, label):
         if not self.graph_mode:
             return self.eager(feature, label)
         if self.graph is None:
-            return self._capture(feature, label)
+            loss, prob = self.eager(feature, label)   # initialises momentum, warms the allocator
+            self._capture_step(feature, label)
+            return loss, prob
         if not self.captured_bn:
             self.bucketer.broadcast_bn()
+        self._load_static(feature, label)
+        self.graph.replay()
+        return self.static[2], self.static[3]
+
+    def _micro_graphed(self, feature, label, last, accum):
+        """Gradient accumulation with graphs (src/trainer.py:280-297 at --accum_step > 1): the non-final micro-step
+        (fwd + bwd of loss / accum under no_sync) and the final one (the same, then the bucket all-reduces, SGD and
+        the gradient zeroing that opens the next window) are captured as two graphs after one eager window, and
+        each micro-step replays one of them.  BatchNorm statistics are broadcast eagerly at each window's start."""
+        if self.agraphs is None:
+            loss, prob = self._micro_eager(feature, label, last, accum)
+            if last:
+                self._capture_accum(feature, label, accum)
+            return loss, prob
+        if self.first_micro:
+            self.bucketer.broadcast_bn()
+            self.first_micro = False
+        self._load_static(feature, label)
+        g, outs = self.agraphs[1] if last else self.agraphs[0]
+        g.replay()
+        if last:
+            self.first_micro = True
+        return outs
+
+    def _load_static(self, feature, label):
         for s, x in zip(self.static[0], feature):
             s.copy_(x, non_blocking=True)
         self.static[1].copy_(label, non_blocking=True)
-        self.graph.replay()
-        return self.static[2], self.static[3]
 
     # capture forms, tried in order (multi-GPU): (bucket all-reduces overlapped with backward, BatchNorm
     # running-stat broadcast inside the graph)
@@ -159,28 +191,17 @@ class TrainStep:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.bucketer.group)
         return bool(flag.item())
 
-    def _capture(self, feature, label):
-        """One eager step (initialises momentum, allocator warm-up), then capture the
-        whole step — grad zeroing, BN broadcast, fwd, bwd, bucket all-reduces, SGD — as one graph.
-        Multi-GPU: the bucket all-reduces are captured where the backward completes each bucket (on the
-        comm stream, overlapping the rest of backward, §8e); if any rank cannot capture that form, every
-        rank retries with one all-reduce pass after backward, then with the BN broadcast outside the graph,
-        and only then do all ranks run eagerly.
+    def _graph(self, body, forms):
+        """Capture body(overlap, bn) -> outputs into a HIP graph under the first form every rank can capture.
         RCCL and the capture: the ProcessGroupNCCL watchdog thread queries the events of eager collectives
         until it retires them, and HIP refuses such a query once the RCCL stream joins a capture (the watchdog
         then aborts the process).  Every capture attempt therefore starts only after GradBucketer.drain has
-        observed, through the flight recorder, that the watchdog retired every eager collective; the
-        capture runs in thread-local mode so no other thread's legal call can invalidate it."""
-        loss, prob = self.eager(feature, label)
-        static_in = [x.clone() for x in feature]
-        static_label = label.clone()
+        observed, through the flight recorder, that the watchdog retired every eager collective; the capture
+        runs in thread-local mode so no other thread's legal call can invalidate it.
+        Returns (graph, outputs, form) or (None, error, None)."""
         err = None
-        forms = self.FORMS if self.bucketer.enabled else ((False, False),)
-        if os.environ.get("DFK_CAPTURE_OVERLAP") == "0":   # probes: only the one-pass forms
-            forms = tuple(f for f in forms if not f[0])
         if self.bucketer.enabled and not recorder_on():   # the same environment on every rank: all go eager
-            forms = ()
-            err = RuntimeError("TORCH_FR_BUFFER_SIZE unset: the RCCL watchdog cannot be observed idle")
+            return None, RuntimeError("TORCH_FR_BUFFER_SIZE unset: the RCCL watchdog cannot be observed idle"), None
         for overlap, bn in forms:
             self.bucketer.drain(self.bucketer.last_works)
             g = torch.cuda.CUDAGraph()
@@ -189,40 +210,82 @@ class TrainStep:
             self.bucketer.overlap = overlap
             self.bucketer.reset()
             self.store.uses.clear()   # a failed attempt may have left forward-use counts behind
-            ok = True
+            ok, outs = True, None
             try:
                 with torch.cuda.stream(s):
                     with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                        self.store.grad.zero_()
-                        self.store.zero_gates()
-                        if bn:
-                            self.bucketer.broadcast_bn()
-                        l2, p2 = self._fwd_bwd(tuple(static_in), static_label)
-                        if overlap:
-                            self.bucketer.finish()         # flush unused buckets, join the comm stream, average
-                        else:
-                            self.bucketer.allreduce_all()
-                        self.opt.step(first=False)
+                        outs = body(overlap, bn)
             except RuntimeError as e:         # e.g. a collective the backend cannot capture in this form
                 torch.cuda.synchronize()
                 err, ok = e, False
             torch.cuda.current_stream().wait_stream(s)
+            self.bucketer.overlap = True
+            self.bucketer.reset()
             if not self._agree(ok):
                 del g
                 continue
-            self.bucketer.overlap = True
-            self.bucketer.reset()
-            self.graph = g
-            self.static = (static_in, static_label, l2, p2)
-            self.captured_overlap = overlap
-            self.captured_bn = bn
-            return loss, prob
-        self.bucketer.overlap = True
-        self.bucketer.reset()
+            return g, outs, (overlap, bn)
+        return None, err, None
+
+    def _step_body(self, static_in, static_label, accum):
+        """The optimizer step's graph body: (zeroing,) BN broadcast, fwd + bwd, all-reduces, SGD."""
+        def body(overlap, bn):
+            if accum == 1:
+                self.store.grad.zero_()
+                self.store.zero_gates()
+                if bn:
+                    self.bucketer.broadcast_bn()
+            l2, p2 = self._fwd_bwd(tuple(static_in), static_label, 1.0 / accum)
+            if overlap:
+                self.bucketer.finish()         # flush unused buckets, join the comm stream, average
+            else:
+                self.bucketer.allreduce_all()
+            self.opt.step(first=False)
+            if accum > 1:                      # the next window starts from zero gradients and gates
+                self.store.grad.zero_()
+                self.store.zero_gates()
+            return l2.detach(), p2.detach()
+        return body
+
+    def _fallback(self, err):
         self.graph_mode = False
         print(f"[deepfake_amd] HIP-graph capture failed ({err}); running the step eagerly", flush=True)
         self.store.zero_grad()
-        return loss, prob
+
+    def _capture_step(self, feature, label):
+        """Capture the whole step — grad zeroing, BN broadcast, fwd, bwd, bucket all-reduces, SGD — as one graph.
+        Multi-GPU: the bucket all-reduces are captured where the backward completes each bucket (on the comm
+        stream, overlapping the rest of backward, §8e); if any rank cannot capture that form, every rank retries
+        with one all-reduce pass after backward, then with the BN broadcast outside the graph, and only then do
+        all ranks run eagerly."""
+        self.static = [[x.clone() for x in feature], label.clone(), None, None]
+        forms = self.FORMS if self.bucketer.enabled else ((False, False),)
+        if os.environ.get("DFK_CAPTURE_OVERLAP") == "0":   # probes: only the one-pass forms
+            forms = tuple(f for f in forms if not f[0])
+        g, outs, form = self._graph(self._step_body(self.static[0], self.static[1], 1), forms)
+        if g is None:
+            return self._fallback(outs)
+        self.graph = g
+        self.static[2], self.static[3] = outs
+        self.captured_overlap, self.captured_bn = form
+
+    def _capture_accum(self, feature, label, accum):
+        """The accumulation window's two graphs (after one eager window: momentum initialised)."""
+        self.static = [[x.clone() for x in feature], label.clone(), None, None]
+
+        def mid(overlap, bn):
+            with self.bucketer.no_sync():
+                l2, p2 = self._fwd_bwd(tuple(self.static[0]), self.static[1], 1.0 / accum)
+            return l2.detach(), p2.detach()
+        gm, outs_m, _ = self._graph(mid, ((False, False),))
+        if gm is None:
+            return self._fallback(outs_m)
+        forms = tuple((o, False) for o in ((True, False) if self.bucketer.enabled else (False,)))
+        gl, outs_l, form = self._graph(self._step_body(self.static[0], self.static[1], accum), forms)
+        if gl is None:
+            return self._fallback(outs_l)
+        self.agraphs = ((gm, outs_m), (gl, outs_l))
+        self.captured_overlap, self.captured_bn = form
 
 
 class Trainer:

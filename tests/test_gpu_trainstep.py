@@ -77,3 +77,29 @@ def test_captured_overlapped_allreduce_single_rank():
     assert "captured overlapped all-reduces: True" in out, out[-3000:]
     assert "captured BN broadcast: True" in out, out[-3000:]
     assert "\nok" in out, out[-3000:]
+
+
+def _run_accum(windows, accum, graph, dt=torch.float32):
+    c = GC.FUSED_C1
+    m = named_fill_(build_fused("c1", compute_dtype=dt), c["seed"]).to(DEV)
+    m.train()
+    store = ParamStore(m, dt)
+    step = TrainStep(m, store, FusedSGD(store, 0.01, 0.9, 0.05), GradBucketer(store), graph=graph)
+    losses = []
+    for i in range(windows * accum):
+        v, mel, w, lab = synthetic_inputs(c["B"], c["T"], c["H"], c["W"], c["seconds"], seed=c["seed"] + 7 * i)
+        loss, _ = step.micro((v.to(DEV), mel.to(DEV), w.to(DEV)), lab.to(DEV), (i + 1) % accum == 0, accum)
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    return store.flat.clone(), losses, step
+
+
+def test_graphed_accumulation_matches_eager():
+    """--accum_step 4 (the reference default, config.py:31; src/trainer.py:280-297) with graphs: one eager window,
+    then the non-final and final micro-step graphs replayed for two more windows — parameters and every
+    micro-step's loss equal the all-eager run (C1, fp32 parity mode)."""
+    ref, lref, _ = _run_accum(3, 4, graph=False)
+    got, lgot, st = _run_accum(3, 4, graph=True)
+    assert st.agraphs is not None and st.graph_mode, "accumulation graphs were not captured"
+    assert max(abs(a - b) for a, b in zip(lgot, lref)) < 1e-5, (lgot, lref)
+    assert _rel(got, ref) < 1e-5

@@ -110,3 +110,23 @@ def test_wattn_bwd(dt, case, table):
     padded = any(n % w for n, w in zip(dims[1:], window))
     if padded:
         chk(torch.cat(dpads), torch.cat([p.grad for p in pr]), "dpad")
+
+
+def test_wattn_bwd_query_chunks():
+    """A window whose Q / dO / dQ exceed the LDS (wav2vec2 at 10 s: T = 499, hd 64 -> Np 512) runs the backward
+    in query chunks, dK / dV accumulated across them (bf16, with attention dropout off and on)."""
+    dims, window, fw, shift, heads, hd = (2, 1, 1, 499), (1, 1, 499), (1, 1, 499), (0, 0, 0), 2, 64
+    g = torch.Generator(device=DEV).manual_seed(9)
+    rows, C = 2 * 499, 2 * 64
+    qkv = torch.randn(rows, 3 * C, device=DEV, generator=g).to(torch.bfloat16)
+    out, lse = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, window, fw, shift, heads, hd, hd ** -0.5)
+    dout = torch.randn(rows, C, device=DEV, generator=g).to(torch.bfloat16)
+    dqkv = torch.empty_like(qkv)
+    K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, 3 * C, dims, window, fw, shift, heads, hd, hd ** -0.5,
+                 None, None), dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C)
+    qr = qkv.float().requires_grad_(True)
+    ref = ref_attention(qr, [torch.zeros(C, device=DEV)] * 3, dims, window, fw, shift, heads, hd, hd ** -0.5, None)
+    assert ((out.float() - ref).abs().max() / ref.abs().max()).item() < 2e-2
+    ref.backward(dout.float())
+    e = ((dqkv.float() - qr.grad).abs().max() / qr.grad.abs().max()).item()
+    assert e < 3e-2, e
