@@ -87,7 +87,7 @@ def time_kernel(fn, iters):
 
 
 ROOFLINE_KERNEL = "wattn_fwd3_kernel<32, true, false>"
-ROOFLINE_PMC = os.path.join(HERE, "profiles", "r3_wattn_fwd_pmc.json")
+ROOFLINE_PMC = os.path.join(HERE, "profiles", "r3f_wattn_fwd_pmc.json")
 
 
 def roofline_case(cfg, B, dt):
