@@ -248,6 +248,14 @@ def cpu_baseline(cfg_name, steps):
                       f"{cores} affinity CPUs"}
 
 
+def workload_name(name, cfg):
+    v = cfg["vst"]
+    trunk = "Swin-B" if v["embed_dim"] == 128 else "Swin-T"
+    ckpt = ", activation-checkpointed video trunk" if v.get("use_checkpoint") else ""
+    return (f"{name.upper()}: {trunk} video {cfg['T']}x{cfg['H']}x{cfg['W']} (window {'x'.join(map(str, v['window_size']))}) + "
+            f"SwinV2 mel 224 + wav2vec2-base {cfg['seconds']}s@16kHz + FusionModel, full train step{ckpt}")
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -317,8 +325,7 @@ def main():
             "metric": METRIC, "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (device-resident, seeded)",
-            "config": {"workload": f"{a.config.upper()}: Swin-T video 32x224x224 (window 8x7x7) + SwinV2 mel 224 + "
-                                   f"wav2vec2-base 4s@16kHz + FusionModel, full train step",
+            "config": {"workload": workload_name(a.config, cfg),
                        "global_batch": world * a.batch, "per_gpu_batch": a.batch,
                        "parallelism": f"dp{world}", "hip_graph": step.graph is not None,
                        "captured_overlap": step.captured_overlap, "captured_bn_broadcast": step.captured_bn,
