@@ -131,6 +131,19 @@ def pmc_traffic():
 
 
 CONV3D_KERNEL = "pe_fwd_kernel<6>"
+CONV3D_INSTEP = os.path.join(HERE, "profiles", "r3i_conv3d_instep.json")
+
+
+def conv3d_in_step():
+    """The same kernel's launches INSIDE the replayed training step, from the committed rocprofv3 kernel trace of
+    this bench command (tools/pe_instep.py separates them from the isolated loop's launches)."""
+    try:
+        with open(CONV3D_INSTEP) as f:
+            d = json.load(f)["in_step"]
+        return {"launches": d["launches"], "median_us": d["median_us"], "achieved_gbs": d["achieved_gbs_median"],
+                "frac": d["frac_median"], "source": os.path.relpath(CONV3D_INSTEP, HERE)}
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
 
 
 def conv3d_roofline(cfg, B, iters, nbuf=3):
@@ -159,7 +172,8 @@ def conv3d_roofline(cfg, B, iters, nbuf=3):
     return {"kernel": CONV3D_KERNEL + " (fused pad + Conv3d 2x4x4 + LayerNorm of the clip batch, cold)",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4), "bytes_per_launch": nbytes, "avg_launch_ms": round(t * 1e3, 4),
-            "timing": f"HIP events over {iters} launches rotating {nbuf} clip batches (working set > Infinity Cache)"}
+            "timing": f"HIP events over {iters} launches rotating {nbuf} clip batches (working set > Infinity Cache)",
+            "in_step": conv3d_in_step() if cfg["T"] == 32 and B == 8 else None}
 
 
 def roofline(cfg, B, dt, iters):

@@ -399,7 +399,15 @@ extern "C" int dfk_patch_embed_fwd(const dfk_patch_embed_args* ap, hipStream_t s
   if (!pe_geo(a, g) || !a.out || !a.mean || !a.rstd || (reinterpret_cast<uintptr_t>(a.out) & 15)) return DFK_EINVAL;
   const long rows = (long)a.B * g.Do * g.Ho;
   const size_t lds = pe_lds_fwd(a.C, g);
-  if (lds > 64 * 1024) return DFK_EINVAL;
+  if (lds > 80 * 1024) return DFK_EINVAL;   // two workgroups per CU
+  static bool attr_set = false;   // C = 128 (Swin-B) needs a little over 64 KB; once per process, never in a capture
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)pe_fwd_kernel<6, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipFuncSetAttribute((const void*)pe_fwd_kernel<6, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipFuncSetAttribute((const void*)pe_fwd_kernel<8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipFuncSetAttribute((const void*)pe_fwd_kernel<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    attr_set = true;
+  }
   // persistent: two workgroups per CU (tuning knobs DFK_PE_PERCU / DFK_PE_DEPTH for tools/pe_bench.py)
   static const int env_cu = getenv("DFK_PE_PERCU") ? atoi(getenv("DFK_PE_PERCU")) : 2;
   static const int depth = getenv("DFK_PE_DEPTH") ? atoi(getenv("DFK_PE_DEPTH")) : 2;

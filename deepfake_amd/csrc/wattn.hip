@@ -719,6 +719,15 @@ __device__ __forceinline__ float selsum(const f32x4& l4, int lane) {
   return r < 16 ? v0 : v1;
 }
 
+// x rounded up (toward +inf) to the nearest bf16 value
+__device__ __forceinline__ float bf16_ceil(float x) {
+  uint32_t u = __float_as_uint(x);
+  const uint32_t lo = u & 0xffffu;
+  u &= 0xffff0000u;
+  if (lo != 0u && !(u >> 31)) u += 0x10000u;   // positive with dropped bits: one bf16 ulp up
+  return __uint_as_float(u);
+}
+
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -738,7 +747,7 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16raw* Ks = reinterpret_cast<bf16raw*>(smem);
   bf16raw* Vs = Ks + (size_t)g.Np * HD;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const WUnit wu = decode_unit(a, g, qsplit);
   const int head = wu.head, win = wu.win, b = wu.b;
@@ -768,6 +777,29 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
     for (int kk = 0; kk < NKK; ++kk)
       qfn[kk] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.q, a.pad_q, qrown, a.ld_qkv, hoff + kk * 16 + hh * 8));
   };
+  // per-lane LDS offsets of the K fragments and of the V^T tr16 reads: the tile swizzle depends on the row
+  // only through (row >> 2) & 3 (hd 32) or row & 3, (row >> 2) & 1 (hd 64), which a key block's 32-row
+  // step and the 16-row k-step leave unchanged, so one offset serves every block (+ kb 32 HD + 16 c HD)
+  int koff[NKK], vlo[NOT], vhi[NOT];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) koff[kk] = swz<HD>(r, kk * 16 + hh * 8);
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot) {
+    const int k0 = 4 * (g16 >> 1) + tq, col = ot * 32 + 16 * (g16 & 1) + 4 * tp;
+    vlo[ot] = swz<HD>(k0, col);
+    vhi[ot] = swz<HD>(k0 + 8, col);
+  }
+  // -m enters the scores as one more MFMA k-step, A[k][slot] = (slot == 0), B[slot][q] = -m (slot 0): m is
+  // kept bf16-representable (rounded up), so the product is exact and the score tile needs no C input copy
+  bf16x8 onesA;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) onesA[j] = (__bf16)(hh == 0 && j == 0 ? 1.f : 0.f);
+  // bias tiles through a buffer descriptor: the lane's 16 B in a VGPR offset, the (qb, kb) tile in an SGPR
+  const uint64_t tp64 = reinterpret_cast<uint64_t>(tch);   // wave-uniform: keep the descriptor in SGPRs
+  const uint64_t tpu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tp64 >> 32)) << 32) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tp64);   // no sign extension
+  const __amdgpu_buffer_rsrc_t trs =
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(tpu), (short)0, TAB ? 0x7fffffff : 0, 0x00020000);
   load_q(min(wu.qpart * nw + wave, nqb - 1));
   for (int qb = wu.qpart * nw + wave; qb < nqb; qb += qstep) {
     const int qrow = qrown;
@@ -778,18 +810,20 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
       for (int j = 0; j < 8; ++j) qf[kk][j] = (__bf16)((float)qfn[kk][j] * qs);
     }
     load_q(min(qb + qstep, nqb - 1));
-    const bf16raw* tq0 = TAB ? tch + (long)qb * nkb * 1024 + lane * 8 : nullptr;   // 1024 bf16 per (qb, kb)
     auto load_bias = [&](bf16x8 (&bt)[2], int kb) {
       if constexpr (TAB) {
+        const int so = __builtin_amdgcn_readfirstlane((qb * nkb + kb) * 2048);   // bytes: 1024 bf16 per (qb, kb)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) bt[c] = *reinterpret_cast<const bf16x8*>(tq0 + (long)kb * 1024 + c * 512);
+        for (int c = 0; c < 2; ++c)
+          bt[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(trs, lane * 16, so + c * 1024, 0));
       }
     };
-    f32x16 o[NOT], mt;
+    f32x16 o[NOT];
     f32x4 l4 = f32x4{0.f, 0.f, 0.f, 0.f};
     float m = 0.f;
+    bf16x8 mB;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) mt[j] = 0.f;
+    for (int j = 0; j < 8; ++j) mB[j] = (__bf16)0.f;
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
@@ -797,13 +831,12 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
     bf16x8 bt[2];
     load_bias(bt, 0);
     auto block = [&](int kb) {
+      const bf16raw* kbase = Ks + kb * 32 * HD;
+      const bf16raw* vbase = Vs + kb * 32 * HD;
       // D = K Q'^T + bias' - m
-      f32x16 d;
+      f32x16 d = mfma32(onesA, mB, f32x16{});
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + swz<HD>(kb * 32 + r, kk * 16 + hh * 8));
-        d = mfma32(kf, qf[kk], kk == 0 ? mt : d);
-      }
+      for (int kk = 0; kk < NKK; ++kk) d = mfma32(*reinterpret_cast<const bf16x8*>(kbase + koff[kk]), qf[kk], d);
       if constexpr (TAB) {
         d = mfma32(bt[0], id0, d);
         d = mfma32(bt[1], id1, d);
@@ -823,11 +856,14 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
       bm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
       const bool grow = kb == 0 || bm > kRescale;
       if (__builtin_amdgcn_ballot_w64(grow) != 0) {
-        const float delta = grow ? bm : 0.f;
+        // m' = m + bm rounded up to a bf16 value: every exponent of this block stays <= 0
+        const float mn = grow ? bf16_ceil(m + bm) : m;
+        const float delta = mn - m;
         const float alpha = kb == 0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
-        m += delta;
+        m = mn;
+        mB[0] = (__bf16)(hh == 0 ? -m : 0.f);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) { d[j] -= delta; mt[j] = -m; }
+        for (int j = 0; j < 16; ++j) d[j] -= delta;
         // the row sums sit in lanes 0-15 (queries 0-15 in register 0, 16-31 in register 1): their factors
         const float a0 = __shfl(alpha, lane & 15, 64), a1 = __shfl(alpha, (lane & 15) + 16, 64);
         l4[0] *= a0;
@@ -857,11 +893,9 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
       // O^T += V^T P^T: A operand rows e = 32 ot + r, k-step c slots 8 hh + j <-> keys 16 c + 8 (j>>2) + 4 hh + (j&3)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const int k0 = kb * 32 + 16 * c + 4 * (g16 >> 1) + tq;
 #pragma unroll
         for (int ot = 0; ot < NOT; ++ot) {
-          const int col = ot * 32 + 16 * (g16 & 1) + 4 * tp;
-          const bf16x8 va = tr16x2(Vs + swz<HD>(k0, col), Vs + swz<HD>(k0 + 8, col));
+          const bf16x8 va = tr16x2(vbase + c * 16 * HD + vlo[ot], vbase + c * 16 * HD + vhi[ot]);
           o[ot] = mfma32(va, pv[c], o[ot]);
         }
         l4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf[c], l4, 0, 0, 0);
@@ -1668,13 +1702,19 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   float* nl2 = reinterpret_cast<float*>(p); p += 4 * Qn;   // -lse log2e; -inf beyond N (P = 0)
   float* ndl = reinterpret_cast<float*>(p); p += 4 * Qn;   // -delta
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const WUnit wu = decode_unit(a, g, 1);   // the forward's work order; lse / dS^T / dropout rows by lse_unit
   const int head = wu.head, win = wu.win, b = wu.b;
   const long unit = wu.lse_unit;
   const int hoff = head * HD;
-  const bf16raw* tch = TAB ? tabb + ((long)wu.cls * a.heads + head) * (long)Np * Np + lane * 8 : nullptr;
+  // bias tiles through a buffer descriptor (wave-uniform base in SGPRs): the lane's 16 B in the VGPR offset,
+  // the (qb, kb) tile in the SGPR offset
+  const uint64_t tp64 = TAB ? reinterpret_cast<uint64_t>(tabb + ((long)wu.cls * a.heads + head) * (long)Np * Np) : 0;
+  const uint64_t tpu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tp64 >> 32)) << 32) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tp64);   // no sign extension
+  const __amdgpu_buffer_rsrc_t trs =
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(tpu), (short)0, TAB ? 0x7fffffff : 0, 0x00020000);
   const float qs = a.scale * kLog2e;
 
   for (int i = tid; i < Np; i += blockDim.x) trow[i] = token_info_row(a, g, b, win, i);
@@ -1709,6 +1749,17 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   bf16raw* Sw = Sd + wave * 32 * kSdRow;
   const DropCtx dc = drop_ctx(a.drop);
   bf16raw* dsu = dsg ? dsg + unit * Np * Np : nullptr;   // this window-head's dS^T [k][q]
+  // per-lane LDS offsets (the tile swizzle sees a row only through bits a 32-row block step and a 16-row
+  // k-step leave unchanged): Q' / dO row fragments (+ qr0 HD) and the transposed tr16 reads (+ qr0 HD + 16 c HD)
+  int qoff[NKK], tlo[NOT], thi[NOT];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) qoff[kk] = swz<HD>(r, kk * 16 + hh * 8);
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot) {
+    const int k0 = 4 * (g16 >> 1) + tq, col = ot * 32 + 16 * (g16 & 1) + 4 * tp;
+    tlo[ot] = swz<HD>(k0, col);
+    thi[ot] = swz<HD>(k0 + 8, col);
+  }
   for (int pass = 0; pass * nw < nkb; ++pass) {
     const int kb = pass * nw + wave;
     if (kb >= nkb) {   // no key block this pass: keep the step barriers
@@ -1741,9 +1792,10 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
     bf16x8 bt[2];
     auto load_bias = [&](int qb) {
       if constexpr (TAB) {
+        const int so = __builtin_amdgcn_readfirstlane(((q0 / 32 + qb) * nkb + kb) * 2048);
 #pragma unroll
         for (int c = 0; c < 2; ++c)
-          bt[c] = *reinterpret_cast<const bf16x8*>(tch + ((long)((q0 / 32 + qb) * nkb + kb) * 2 + c) * 512);
+          bt[c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(trs, lane * 16, so + c * 1024, 0));
       }
     };
     int qb = wave % nqb;
@@ -1758,13 +1810,13 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
         const f32x4 d4 = *reinterpret_cast<const f32x4*>(ndl + qr0 + 8 * v + 4 * hh);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          s[4 * v + t] = l4[t] + kneg;
+          s[4 * v + t] = TAB ? l4[t] : l4[t] + kneg;   // the bias tiles hold -1e4 for keys beyond N
           dp[4 * v + t] = DROP ? 0.f : d4[t];
         }
       }
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
-        const int off = swz<HD>(qr0 + r, kk * 16 + hh * 8);
+        const int off = qr0 * HD + qoff[kk];
         const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + off);
         const bf16x8 da = *reinterpret_cast<const bf16x8*>(dOs + off);
         s = mfma32(qa, kB[kk], s);
@@ -1802,12 +1854,11 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
       // dV^T += dO^T P, dK^T += Q'^T dS: A rows e = 32 ot + r, k-step c slots <-> queries 16 c + 8 (j>>2) + 4 hh + (j&3)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const int qr = qr0 + 16 * c + 4 * (g16 >> 1) + tq;
+        const int rb = (qr0 + 16 * c) * HD;
 #pragma unroll
         for (int ot = 0; ot < NOT; ++ot) {
-          const int col = ot * 32 + 16 * (g16 & 1) + 4 * tp;
-          const bf16x8 doT = tr16x2(dOs + swz<HD>(qr, col), dOs + swz<HD>(qr + 8, col));
-          const bf16x8 qT = tr16x2(Qs + swz<HD>(qr, col), Qs + swz<HD>(qr + 8, col));
+          const bf16x8 doT = tr16x2(dOs + rb + tlo[ot], dOs + rb + thi[ot]);
+          const bf16x8 qT = tr16x2(Qs + rb + tlo[ot], Qs + rb + thi[ot]);
           dVt[ot] = mfma32(doT, pa[c], dVt[ot]);
           dKt[ot] = mfma32(qT, sa[c], dKt[ot]);
         }

@@ -73,7 +73,7 @@ def test_patch_embed(dt):
 
 
 @pytest.mark.parametrize("shape,layout,C", [((2, 3, 8, 32, 32), "bcthw", 96), ((1, 32, 3, 224, 224), "btchw", 96),
-                                            ((1, 7, 3, 30, 44), "btchw", 128)])
+                                            ((1, 7, 3, 30, 44), "btchw", 128), ((1, 4, 3, 224, 224), "btchw", 128)])
 def test_patch_embed_fused_matches_unfused(shape, layout, C):
     """The fused bf16 pad + Conv3d + LayerNorm kernel (dfk_patch_embed_fwd/bwd) against the three-pass
     path (im2col -> GEMM -> LN) on the same inputs: C2 clip geometry in place ([B,T,3,H,W]), padded T/H/W,

@@ -23,3 +23,5 @@ head -24 $OUT/kernel_summary.txt
 python3 tools/pe_instep.py $(find $OUT/trace -name 'run_kernel_trace.csv' | head -1) $OUT/${TAG}_conv3d_instep.json
 timeout -k 10 600 python3 -u bench.py --config c5 --batch 4 --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { tail -30 $OUT/bench_c5.err; exit 1; }
 cat $OUT/bench_c5.json
+timeout -k 10 600 python3 -u bench.py --config c4 --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_c4.json 2> $OUT/bench_c4.err || { tail -30 $OUT/bench_c4.err; exit 1; }
+cat $OUT/bench_c4.json
