@@ -131,7 +131,7 @@ def pmc_traffic():
 
 
 CONV3D_KERNEL = "pe_fwd_kernel<6>"
-CONV3D_INSTEP = os.path.join(HERE, "profiles", "r3i_conv3d_instep.json")
+CONV3D_INSTEP = os.path.join(HERE, "profiles", "r3j_conv3d_instep.json")
 
 
 def conv3d_in_step():

@@ -753,11 +753,32 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
   const int head = wu.head, win = wu.win, b = wu.b;
   const long unit = wu.lse_unit;
   const int hoff = head * HD;
-  for (int idx = tid; idx < g.Np * CH; idx += blockDim.x) {
-    const int i = idx / CH, c = (idx % CH) * 8;
-    const int row = token_info_row(a, g, b, win, i);
-    *reinterpret_cast<uint4*>(Ks + swz<HD>(i, c)) = tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + c);
-    *reinterpret_cast<uint4*>(Vs + swz<HD>(i, c)) = tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + c);
+  // K / V gather, KV_B chunks per thread in flight: every load of a batch is issued (clamped, branch-free
+  // addresses) before the one wait that precedes its LDS writes — a load / wait / write chain per chunk
+  // costs one HBM round trip each (7 K + 7 V per thread at Np 416)
+  {
+    constexpr int KV_B = 4;
+    const int tot = g.Np * CH;
+    for (int base = tid; base < tot; base += KV_B * blockDim.x) {
+      uint4 kv[KV_B], vv[KV_B];
+      int off[KV_B];
+#pragma unroll
+      for (int u = 0; u < KV_B; ++u) {
+        const int idx = min(base + u * (int)blockDim.x, tot - 1);
+        const int i = idx / CH, c = (idx % CH) * 8;
+        const int row = token_info_row(a, g, b, win, i);
+        off[u] = swz<HD>(i, c);
+        kv[u] = tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + c);
+        vv[u] = tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + c);
+      }
+#pragma unroll
+      for (int u = 0; u < KV_B; ++u) {
+        if (base + u * (int)blockDim.x < tot) {
+          *reinterpret_cast<uint4*>(Ks + off[u]) = kv[u];
+          *reinterpret_cast<uint4*>(Vs + off[u]) = vv[u];
+        }
+      }
+    }
   }
   const int nkb = g.Np / 32, nqb = g.Np / 32;
   const bf16raw* tch = TAB ? tab + ((long)wu.cls * a.heads + head) * (long)g.Np * g.Np : nullptr;
@@ -1722,25 +1743,39 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
     nl2[i] = q0 + i < g.N ? -a.lse[unit * Np + q0 + i] * kLog2e : -INFINITY;
   for (int i = tid * 4; i < Qn * HD; i += blockDim.x * 4) *reinterpret_cast<f32x4*>(dQa + i) = f32x4{0, 0, 0, 0};
   __syncthreads();
-  for (int base = 0; base < Qn * CH; base += blockDim.x) {
-    const int idx = base + tid;
-    float d = 0.f;
-    if (idx < Qn * CH) {
-      const int li = idx / CH, c = (idx % CH) * 8;
-      const int row = trow[q0 + li];
-      uint4 qv = tok_ld16<bf16raw>(a.q, a.pad_q, row, a.ld_qkv, hoff + c);
-      const uint4 dv = tok_ld16<bf16raw>(ba.dout, nullptr, row, ba.ld_dout, hoff + c);
-      const uint4 ov = tok_ld16<bf16raw>(a.out, nullptr, row, a.ld_out, hoff + c);
-      d = dot8_bf16(ov, dv);
-      bf16x8 qb8 = __builtin_bit_cast(bf16x8, qv);
+  // Q / dO / O gather, QB row chunks per thread in flight (all loads of a batch issued before the wait that
+  // precedes their use: one HBM round trip per batch, not per chunk)
+  {
+    constexpr int QB = 4;
+    const int tot = Qn * CH;
+    for (int base = 0; base < tot; base += QB * blockDim.x) {
+      uint4 qv[QB], dv[QB], ov[QB];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qb8[j] = (__bf16)((float)qb8[j] * qs);   // the forward's Q' rounding, bit for bit
-      *reinterpret_cast<bf16x8*>(Qs + swz<HD>(li, c)) = qb8;
-      *reinterpret_cast<uint4*>(dOs + swz<HD>(li, c)) = dv;
+      for (int u = 0; u < QB; ++u) {
+        const int idx = min(base + u * (int)blockDim.x + tid, tot - 1);
+        const int li = idx / CH, c = (idx % CH) * 8;
+        const int row = trow[q0 + li];
+        qv[u] = tok_ld16<bf16raw>(a.q, a.pad_q, row, a.ld_qkv, hoff + c);
+        dv[u] = tok_ld16<bf16raw>(ba.dout, nullptr, row, ba.ld_dout, hoff + c);
+        ov[u] = tok_ld16<bf16raw>(a.out, nullptr, row, a.ld_out, hoff + c);
+      }
+#pragma unroll
+      for (int u = 0; u < QB; ++u) {
+        const int idx = base + u * (int)blockDim.x + tid;   // CH | blockDim: a row's CH lanes agree on idx < tot
+        float d = dot8_bf16(ov[u], dv[u]);
+#pragma unroll
+        for (int o = 1; o < CH; o <<= 1) d += __shfl_xor(d, o, 64);
+        if (idx < tot) {
+          const int li = idx / CH, c = (idx % CH) * 8;
+          bf16x8 qb8 = __builtin_bit_cast(bf16x8, qv[u]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) qb8[j] = (__bf16)((float)qb8[j] * qs);   // the forward's Q' rounding, bit for bit
+          *reinterpret_cast<bf16x8*>(Qs + swz<HD>(li, c)) = qb8;
+          *reinterpret_cast<uint4*>(dOs + swz<HD>(li, c)) = dv[u];
+          if ((idx % CH) == 0) ndl[li] = -d;
+        }
+      }
     }
-#pragma unroll
-    for (int o = 1; o < CH; o <<= 1) d += __shfl_xor(d, o, 64);
-    if (idx < Qn * CH && (idx % CH) == 0) ndl[idx / CH] = -d;
   }
   __syncthreads();
 

@@ -60,11 +60,14 @@ def main():
         tb = timed(lambda: K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, 3 * C, dims, win, fw, shift, heads,
                                         hd, scale, rpb, None), dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C,
                                        drpb=drpb, tab=tab))
+        tb0 = timed(lambda: K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, 3 * C, dims, win, fw, shift, heads,
+                                         hd, scale, rpb, None), dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C,
+                                        drpb=None, tab=tab)) if rpb is not None else float("nan")
         units = dims[0] * nW * heads
         ff = 4.0 * units * N * N * hd
         fb = 10.0 * units * N * N * hd
         print(f"{name:8s} units {units:6d} N {N:4d} fwd {tf:8.1f} us {ff / tf / 1e6:7.1f} TF/s | "
-              f"bwd {tb:8.1f} us {fb / tb / 1e6:7.1f} TF/s", flush=True)
+              f"bwd {tb:8.1f} us {fb / tb / 1e6:7.1f} TF/s (no dRPB {tb0:7.1f} us)", flush=True)
 
 
 if __name__ == "__main__":
