@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void rowmean_kernel(const T* __restrict__ x, T
 template <typename T>
 __global__ void gelu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ pre, T* __restrict__ dx, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) stf<T>(dx + i, ldf<T>(dy + i) * dgelu_f(ldf<T>(pre + i)));
+  if (i < n) stf<T>(dx + i, ldf<T>(dy + i) * (sizeof(T) == 2 ? dgelu_bf(ldf<T>(pre + i)) : dgelu_f(ldf<T>(pre + i))));
 }
 
 template <typename TI, typename TO>

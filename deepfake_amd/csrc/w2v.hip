@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void conv0_apply(const float* __restrict__ x, 
     const int tl = i / CH, c = i % CH;
     const float y = conv_at(xs, ws, tl, c);
     const float z = (y - mu[c]) * rs[c] * gamma[c] + beta[c];
-    stf<T>(out + ((long)b * T0 + t0 + tl) * CH + c, gelu_f(z));
+    stf<T>(out + ((long)b * T0 + t0 + tl) * CH + c, (sizeof(T) == 2 ? gelu_bf(z) : gelu_f(z)));
   }
 }
 
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void conv0_bwd_stats(const float* __restrict__
     float A = 0.f, Bs = 0.f;
     for (int tl = 0; tl < nt; ++tl) {
       const float yh = (conv_at(xs, ws, tl, c) - m) * r;
-      const float dz = ldf<T>(dout + ((long)b * T0 + t0 + tl) * CH + c) * dgelu_f(yh * gamma[c] + beta[c]);
+      const float dz = ldf<T>(dout + ((long)b * T0 + t0 + tl) * CH + c) * (sizeof(T) == 2 ? dgelu_bf(yh * gamma[c] + beta[c]) : dgelu_f(yh * gamma[c] + beta[c]));
       A += dz * yh;
       Bs += dz;
     }
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void conv0_bwd_dw(const float* __restrict__ x,
       for (int j = 0; j < CPT; ++j) {
         const int c = threadIdx.x + j * 256;
         const float yh = (conv_at(xs, ws, tl, c) - m[j]) * r[j];
-        const float dz = ldf<T>(dout + ((long)b * T0 + t0 + tl) * CH + c) * dgelu_f(yh * g[j] + be[j]);
+        const float dz = ldf<T>(dout + ((long)b * T0 + t0 + tl) * CH + c) * (sizeof(T) == 2 ? dgelu_bf(yh * g[j] + be[j]) : dgelu_f(yh * g[j] + be[j]));
         const float dy = r[j] * (g[j] * dz - Bm[j] - yh * A[j]);
 #pragma unroll
         for (int k = 0; k < KW; ++k) acc[j][k] += dy * xs[tl * KS + k];

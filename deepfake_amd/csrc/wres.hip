@@ -209,11 +209,11 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
         bias4(nb, v);
         if constexpr (ACT == 1) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+          for (int e = 0; e < 4; ++e) v[e] = gelu_bf(v[e]);
         } else if constexpr (ACT == 2) {
           const uint2 a = ax[nb];
-          v[0] *= dgelu_f(__uint_as_float(a.x << 16)); v[1] *= dgelu_f(__uint_as_float(a.x & 0xffff0000u));
-          v[2] *= dgelu_f(__uint_as_float(a.y << 16)); v[3] *= dgelu_f(__uint_as_float(a.y & 0xffff0000u));
+          v[0] *= dgelu_bf(__uint_as_float(a.x << 16)); v[1] *= dgelu_bf(__uint_as_float(a.x & 0xffff0000u));
+          v[2] *= dgelu_bf(__uint_as_float(a.y << 16)); v[3] *= dgelu_bf(__uint_as_float(a.y & 0xffff0000u));
         }
         if (dc.mode == 2) {
 #pragma unroll
