@@ -110,8 +110,15 @@ def test_c5_long_clip_checkpointed():
         return ((x - y).abs().max() / y.abs().max().clamp_min(1e-12)).item()
     # bar: 2e-2 (bf16), or 3x the run-to-run spread of the un-checkpointed model itself for tensors whose
     # gradient is a near-cancelling sum (order-dependent fp32 atomics upstream, then bf16 rounding)
+    # tensors whose gradient is analytically zero (attention key biases: softmax is invariant to a per-query
+    # shift, so d/db_k = sum_q q (sum_k dS) = 0) hold bf16 rounding noise only: relative errors of noise are
+    # meaningless there, so they are held to an absolute bound against the model's largest gradient instead
+    top = max(float(g.abs().max()) for g in gb.values())
     for n in gb:
         e, noise = rel(ga[n], gb[n]), rel(gb2[n], gb[n])
+        if noise > 0.5 or float(gb[n].abs().max()) < 1e-4 * top:   # noise-dominated: analytically zero
+            assert float(ga[n].abs().max()) < 1e-3 * top, (n, float(ga[n].abs().max()), top)
+            continue
         assert e <= max(2e-2, 3 * noise), (n, e, noise)
     print(f"C5 B=2 peak activation memory: checkpointed {pa / 2**30:.2f} GiB, plain {pb / 2**30:.2f} GiB")
     assert pa < pb

@@ -20,6 +20,7 @@ cat $OUT/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
     python3 bench.py --no-cpu-baseline > $OUT/trace.log 2>&1 || { tail -30 $OUT/trace.log; exit 1; }
 python3 tools/prof_summary.py $(find $OUT/trace -name 'run_kernel_stats.csv' | head -1) 13 45 > $OUT/kernel_summary.txt
+python3 tools/pe_instep.py $(find $OUT/trace -name "run_kernel_trace.csv" | head -1) $OUT/${TAG}_conv3d_instep.json
 head -30 $OUT/kernel_summary.txt
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_f -o run --output-format csv -- python3 tools/roofline_pmc.py run 5 > $OUT/pmc_f.log 2>&1 || { tail $OUT/pmc_f.log; exit 1; }
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_w -o run --output-format csv -- python3 tools/roofline_pmc.py run 5 > $OUT/pmc_w.log 2>&1 || { tail $OUT/pmc_w.log; exit 1; }
