@@ -107,6 +107,30 @@ __device__ __forceinline__ float phi_cdf_bf(float x, float& e) {
   return x >= 0.f ? fmaf(-0.5f, ec, 1.f) : 0.5f * ec;
 }
 __device__ __forceinline__ float gelu_bf(float x) { float e; return x * phi_cdf_bf(x, e); }
+
+// The same on a pair of values in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two elements per VALU issue;
+// the reciprocal and the exp stay per element)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 phi_cdf_bf2(f32x2 x, f32x2& e) {
+  const f32x2 t = f32x2{fabsf(x.x), fabsf(x.y)} * 0.70710678118654752f;
+  const f32x2 den = t * 0.3275911f + 1.f;
+  const f32x2 k = f32x2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f32x2 y = k * 1.061405429f - 1.453152027f;
+  y = k * y + 1.421413741f;
+  y = k * y - 0.284496736f;
+  y = k * y + 0.254829592f;
+  const f32x2 tt = t * t * -1.4426950408889634f;
+  e = f32x2{__builtin_amdgcn_exp2f(tt.x), __builtin_amdgcn_exp2f(tt.y)};
+  const f32x2 ec = k * y * e;   // erfc(t)
+  const f32x2 hi = ec * -0.5f + 1.f, lo = ec * 0.5f;
+  return f32x2{x.x >= 0.f ? hi.x : lo.x, x.y >= 0.f ? hi.y : lo.y};
+}
+__device__ __forceinline__ f32x2 gelu_bf2(f32x2 x) { f32x2 e; return x * phi_cdf_bf2(x, e); }
+__device__ __forceinline__ f32x2 dgelu_bf2(f32x2 x) {
+  f32x2 e;
+  const f32x2 p = phi_cdf_bf2(x, e);
+  return x * 0.3989422804014327f * e + p;
+}
 __device__ __forceinline__ float dgelu_bf(float x) {
   float e;
   const float p = phi_cdf_bf(x, e);

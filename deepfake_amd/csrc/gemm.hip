@@ -173,12 +173,28 @@ __device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1
   if (g.act == 1) {
     T* ap = aux ? aux + (long)row * g.ldaux + col0 : nullptr;
     if (ap) { if (full) st8<T>(ap, v); else for (int e = 0; e < 8; ++e) if (e < ncol) stf<T>(ap + e, v[e]); }
-    for (int e = 0; e < 8; ++e) v[e] = sizeof(T) == 2 ? gelu_bf(v[e]) : gelu_f(v[e]);
+    if constexpr (sizeof(T) == 2) {
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2 r = gelu_bf2(f32x2{v[e], v[e + 1]});
+        v[e] = r.x;
+        v[e + 1] = r.y;
+      }
+    } else {
+      for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+    }
   } else if (g.act == 2) {
     const T* ap = aux + (long)row * g.ldaux + col0;
     float a8[8];
     if (full) ld8<T>(ap, a8); else for (int e = 0; e < 8; ++e) if (e < ncol) a8[e] = ldf<T>(ap + e);
-    for (int e = 0; e < 8; ++e) v[e] *= sizeof(T) == 2 ? dgelu_bf(a8[e]) : dgelu_f(a8[e]);
+    if constexpr (sizeof(T) == 2) {
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2 d = dgelu_bf2(f32x2{a8[e], a8[e + 1]});
+        v[e] *= d.x;
+        v[e + 1] *= d.y;
+      }
+    } else {
+      for (int e = 0; e < 8; ++e) v[e] *= dgelu_f(a8[e]);
+    }
   }
   if (g.drop.mode && g.drop.rng) {   // dropout / DropPath of the branch output (before the residual add)
     const DropCtx dc = drop_ctx(g.drop);

@@ -209,11 +209,16 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
         bias4(nb, v);
         if constexpr (ACT == 1) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_bf(v[e]);
+          for (int e = 0; e < 4; e += 2) {
+            const f32x2 r = gelu_bf2(f32x2{v[e], v[e + 1]});
+            v[e] = r.x;
+            v[e + 1] = r.y;
+          }
         } else if constexpr (ACT == 2) {
           const uint2 a = ax[nb];
-          v[0] *= dgelu_bf(__uint_as_float(a.x << 16)); v[1] *= dgelu_bf(__uint_as_float(a.x & 0xffff0000u));
-          v[2] *= dgelu_bf(__uint_as_float(a.y << 16)); v[3] *= dgelu_bf(__uint_as_float(a.y & 0xffff0000u));
+          const f32x2 d0 = dgelu_bf2(f32x2{__uint_as_float(a.x << 16), __uint_as_float(a.x & 0xffff0000u)});
+          const f32x2 d1 = dgelu_bf2(f32x2{__uint_as_float(a.y << 16), __uint_as_float(a.y & 0xffff0000u)});
+          v[0] *= d0.x; v[1] *= d0.y; v[2] *= d1.x; v[3] *= d1.y;
         }
         if (dc.mode == 2) {
 #pragma unroll
