@@ -316,8 +316,8 @@ def patch_merge(x, dims, reverse=False, out=None):
     B, D, H, W = dims
     C = x.shape[1] if not reverse else x.shape[1] // 4
     if out is None:
-        if reverse:
-            out = torch.zeros(B * D * H * W, C, device=x.device, dtype=x.dtype)
+        if reverse:   # every un-merged token belongs to exactly one merged row: the kernel writes all of out
+            out = torch.empty(B * D * H * W, C, device=x.device, dtype=x.dtype)
         else:
             out = torch.empty(B * D * ((H + 1) // 2) * ((W + 1) // 2), 4 * C, device=x.device, dtype=x.dtype)
     L.check(L.lib().dfk_patch_merge(L.ptr(x), L.ptr(out), B, D, H, W, C, int(reverse), L.dt(x), L.stream()),
