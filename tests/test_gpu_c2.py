@@ -176,3 +176,25 @@ def test_fused_c1_grad_tensors(dt):
     assert abs(loss.item() - float(fx["loss"])) < LOGIT_TOL[dt] * abs(float(fx["loss"]))
     check_grads(fx, dict(m.named_parameters()), GRAD_TOL[dt], what="c1 ",
                 ref_factor=BF16_REF_FACTOR if dt == torch.bfloat16 else None)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fused_c2_b8_eval_logits_vs_oracle(dt):
+    """The bench's own batch (C2 at B = 8, the goldens hold B = 2): eval logits of the HIP path against the
+    oracle (fp32 CPU restatement of the reference, pinned to the goldens) on the same weights and inputs —
+    1e-3 relative in fp32 parity mode (the north-star bar), 2e-2 in bf16."""
+    from deepfake_amd.models.fused import CONFIGS, W2V_CONFIG
+    from oracle import fusion as OF
+    cfg = CONFIGS["c2"]
+    m = named_fill_(build_fused("c2", compute_dtype=dt), 21).to(DEV)
+    ref = named_fill_(OF.build_fused(cfg, W2V_CONFIG), 21)
+    video, mel, wave, _ = synthetic_inputs(8, cfg["T"], cfg["H"], cfg["W"], cfg["seconds"], seed=22)
+    m.eval()
+    ref.eval()
+    with torch.no_grad():
+        m((video.to(DEV), mel.to(DEV), wave.to(DEV)))
+        ref((video, mel, wave))
+    z, zr = m.last_logits.float().cpu().numpy(), ref.last_logits.numpy()
+    err = _logit_err(z, zr)
+    print(f"C2 B=8 eval logits rel err vs oracle {err:.3e} ({dt})")
+    assert z.shape == zr.shape and err < LOGIT_TOL[dt], (z, zr, err)
