@@ -253,25 +253,31 @@ def test_layerdrop_gate_is_or_over_accumulation_window():
     from deepfake_amd.optim import FusedSGD
     from deepfake_amd.params import ParamStore
     torch.manual_seed(0)
-    rng.manual_seed(11, 0)
     cfg = Wav2Vec2Config.from_json_file(W2V_CONFIG, num_hidden_layers=8).deterministic()
     cfg.layerdrop = 0.5
     enc = set_compute_dtype(Wav2Vec2Encoder(cfg), torch.float32).to(DEV).train()
     store = ParamStore(enc, torch.float32)
-    store.zero_grad()
     opt = FusedSGD(store, 0.1, 0.9, 0.05)
     g = torch.Generator(device=DEV).manual_seed(3)
     h = torch.randn(2, 49, 768, device=DEV, generator=g)
     wy = torch.randn(2, 49, 768, device=DEV, generator=g)
-    coins = []
-    for _ in range(4):
-        rng.advance(DEV)
-        (enc(h).float() * wy).sum().backward()
-        coins.append(enc.layer_keep.clone())
-    c = torch.stack(coins)
-    used = c.amax(0)
+    # the coins depend on the LayerDrop site id, i.e. on how many dropout sites earlier tests created: take the
+    # first seed whose window has a layer kept in an earlier micro-step and dropped in the last one
+    for seed in range(11, 43):
+        rng.manual_seed(seed, 0)
+        store.zero_grad()
+        coins = []
+        for _ in range(4):
+            rng.advance(DEV)
+            (enc(h).float() * wy).sum().backward()
+            coins.append(enc.layer_keep.clone())
+        c = torch.stack(coins)
+        used = c.amax(0)
+        if bool(((c[-1] == 0) & (used == 1)).any()):
+            break
+    else:
+        pytest.fail("no seed in 11..42 exercises kept-then-dropped")
     assert torch.equal(enc.layer_used, used)
-    assert bool(((c[-1] == 0) & (used == 1)).any()), "seed must exercise kept-then-dropped"
     p0, g0 = store.flat.clone(), store.grad.clone()
     opt.step()
     for i, layer in enumerate(enc.layers):
