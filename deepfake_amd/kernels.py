@@ -91,7 +91,7 @@ def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None, residual=No
     return out
 
 
-_DW_MIN_K = int(os.environ.get("DFK_DW_MINK", "256"))   # tokens per split of a weight-gradient GEMM (tuning)
+_DW_MIN_K = int(os.environ.get("DFK_DW_MINK", "512"))   # tokens per split of a weight-gradient GEMM (tuning)
 _DW_SLAB_MAX = int(os.environ.get("DFK_DW_SLAB_MAX", "16"))          # slab (non-atomic) split-K bounds (tuning)
 _DW_SLAB_BYTES = int(os.environ.get("DFK_DW_SLAB_BYTES", str(16 << 20)))
 
