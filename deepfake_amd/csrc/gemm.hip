@@ -814,7 +814,8 @@ int auto_splitk(const dfk_gemm_args& g) {
   // the shorter k-loop saves (C2 sweep of the LDS-DMA kernel: K = 512-2048 run fastest unsplit, K >= 2304
   // with 3-4 splits)
   const int maxs = g.K / (12 * TBK);
-  const int want = (int)dfk_cdiv(768, tiles);
+  static const int target = getenv("DFK_GEMM_SPLIT_TARGET") ? atoi(getenv("DFK_GEMM_SPLIT_TARGET")) : 768;   // tuning runs only
+  const int want = (int)dfk_cdiv(target, tiles);
   return std::max(1, std::min(maxs, want));
 }
 

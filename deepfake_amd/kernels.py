@@ -11,7 +11,10 @@ import torch
 
 from . import _lib as L
 
-_CU_TARGET_BLOCKS = 512  # split-K target grid for skinny weight-gradient GEMMs (2 per CU; fewer atomics)
+# split-K target grid of a skinny weight-gradient GEMM: 128 workgroups.  In isolation 512 (two per CU) runs each
+# dW fastest, but inside the step the other two branch streams fill the chip and fewer splits mean fewer fp32
+# partials (whole-step A/B: 512 -> 256 -> 128 = 241.7 -> 244.8 -> 245.3 clips/s; 64: 232.7)
+_CU_TARGET_BLOCKS = int(os.environ.get("DFK_DW_TARGET", "128"))
 
 
 def _view(t, ld, bs0=0, bs1=0, conv=None):
