@@ -95,8 +95,6 @@ def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None, residual=No
 
 
 _DW_MIN_K = int(os.environ.get("DFK_DW_MINK", "512"))   # tokens per split of a weight-gradient GEMM (tuning)
-_DW_SLAB_MAX = int(os.environ.get("DFK_DW_SLAB_MAX", "16"))          # slab (non-atomic) split-K bounds (tuning)
-_DW_SLAB_BYTES = int(os.environ.get("DFK_DW_SLAB_BYTES", str(16 << 20)))
 
 
 def splitk_for(tiles, K, min_k=None):
@@ -119,13 +117,6 @@ def linear_dw(dy, x, dw, db=None):
     # fp32 partial bytes (splits x N x K x 4) kept to a quarter of the operand bytes read, except that small
     # grids keep up to 8 splits for parallelism (C2 sweep: mel1.fc1 [25088]x512x128 98 -> 30 splits, 42 -> 28 us)
     s = max(1, min(s, max(8, M * (N + K) // (8 * N * K))))
-    if s <= _DW_SLAB_MAX and s * N * K * 4 >= _DW_SLAB_BYTES:
-        # few splits over a large output: fp32 slabs + one reduce pass (plain stores, beta=1 accumulate) beat
-        # same-address atomics there (C2 sweep: vst3.fc1 / fc2 dW 63 -> 56, 66 -> 59 us); with many splits
-        # (huge-M) or a small output the atomics win (reduce launch, serial sum over the splits)
-        gemm(dy, dy.stride(0), True, x, x.stride(0), True, N, K, M, dw, dw.stride(0), dtype=L.dt(dy), c_f32=True,
-             beta=1.0, splitk=s, rowsum=db)
-        return dw
     gemm(dy, dy.stride(0), True, x, x.stride(0), True, N, K, M, dw, dw.stride(0), dtype=L.dt(dy), c_f32=True,
          atomic=s > 1, beta=1.0, splitk=s, rowsum=db)
     return dw
