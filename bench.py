@@ -87,7 +87,7 @@ def time_kernel(fn, iters):
 
 
 ROOFLINE_KERNEL = "wattn_fwd3_kernel<32, true, false>"
-ROOFLINE_PMC = os.path.join(HERE, "profiles", "r3n_wattn_fwd_pmc.json")
+ROOFLINE_PMC = os.path.join(HERE, "profiles", "r3o_wattn_fwd_pmc.json")
 
 
 def roofline_case(cfg, B, dt):
@@ -131,7 +131,7 @@ def pmc_traffic():
 
 
 CONV3D_KERNEL = "pe_fwd_kernel<6>"
-CONV3D_INSTEP = os.path.join(HERE, "profiles", "r3n_conv3d_instep.json")
+CONV3D_INSTEP = os.path.join(HERE, "profiles", "r3o_conv3d_instep.json")
 
 
 def conv3d_in_step():
