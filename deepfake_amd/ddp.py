@@ -32,19 +32,42 @@ def recorder_on():
     return max(int(os.environ.get(k, "0") or 0) for k in ("TORCH_FR_BUFFER_SIZE", "TORCH_NCCL_TRACE_BUFFER_SIZE")) > 0
 
 
-def watchdog_idle(timeout=60.0):
+def _fr_dumps():
+    """The flight-recorder dump functions of this torch build (the NCCL/RCCL recorder and the generic one used
+    by gloo are separate).  Raises when neither exists: without them the watchdog cannot be observed idle, and
+    a capture that starts while it still polls an eager collective aborts the process."""
+    from torch._C import _distributed_c10d as c10d
+    dumps = [getattr(c10d, n) for n in ("_dump_nccl_trace_json", "_dump_fr_trace_json") if hasattr(c10d, n)]
+    if not dumps:
+        raise RuntimeError("this torch build exposes no flight-recorder dump (_dump_nccl_trace_json / "
+                           "_dump_fr_trace_json): the RCCL watchdog cannot be observed idle")
+    return dumps
+
+
+def fr_entries():
+    import json
+    return [e for dump in _fr_dumps() for e in json.loads(dump(includeCollectives=True, onlyActive=False))
+            .get("entries") or []]
+
+
+def fr_last_id():
+    """Highest flight-recorder record id so far (-1: none); brackets the collectives of one capture attempt."""
+    return max((int(e.get("record_id", -1)) for e in fr_entries()), default=-1)
+
+
+def watchdog_idle(timeout=60.0, exclude=()):
     """Wait until the flight recorder lists every collective as retired: the ProcessGroupNCCL watchdog marks a
     work retired in the same critical section in which it drops the work from the list it polls, so after that
-    it queries none of their events again.  Raises on timeout."""
-    import json
+    it queries none of their events again.  exclude: (lo, hi] record-id ranges of collectives recorded during a
+    failed capture attempt (captured, never run: the watchdog never retires them).  Raises on timeout, and when
+    the torch build has no flight recorder to poll."""
     import time
-    from torch._C import _distributed_c10d as c10d
-    # the NCCL (RCCL) recorder and the generic one (gloo) are separate
-    dumps = [getattr(c10d, n) for n in ("_dump_nccl_trace_json", "_dump_fr_trace_json") if hasattr(c10d, n)]
+    _fr_dumps()
     t0 = time.monotonic()
     polls = 0
     while True:
-        ents = [e for dump in dumps for e in json.loads(dump(includeCollectives=True, onlyActive=False)).get("entries") or []]
+        ents = [e for e in fr_entries()
+                if not any(lo < int(e.get("record_id", -1)) <= hi for lo, hi in exclude)]
         live = [e for e in ents if not e.get("retired", False)]
         polls += 1
         if os.environ.get("DFK_DEBUG_WATCHDOG") and (polls == 1 or not live):
@@ -98,6 +121,7 @@ class GradBucketer:
         if self.enabled and comm_dtype != torch.float32:
             self.cbuf = torch.zeros(store.grad.numel(), dtype=comm_dtype, device=store.grad.device)
         self.last_works = []      # the previous eager step's bucket works (drained before a graph capture)
+        self.fr_exclude = []      # flight-recorder id ranges of failed capture attempts (see watchdog_idle)
         if self.enabled:
             for i, p in enumerate(store.params):
                 self.hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -172,8 +196,12 @@ class GradBucketer:
             w.wait()
         if self.store.grad.is_cuda:
             torch.cuda.synchronize()
-        if self.enabled and self.store.grad.is_cuda and recorder_on():
-            watchdog_idle(timeout)
+        if self.watched():
+            watchdog_idle(timeout, exclude=self.fr_exclude)
+
+    def watched(self):
+        """A capture here needs the watchdog drain (RCCL on the device, flight recorder on)."""
+        return self.enabled and self.store.grad.is_cuda and recorder_on()
 
     def finish(self):
         """After the last micro-step's backward: flush buckets not yet launched (unused

@@ -15,6 +15,7 @@ re-built MI355X-first:
   step at :133,136);
 * optional HIP-graph capture of the whole step (TrainStep(graph=True)).
 """
+import math
 import os
 import time
 
@@ -22,7 +23,7 @@ import torch
 import torch.distributed as dist
 
 from . import rng
-from .ddp import GradBucketer, recorder_on
+from .ddp import GradBucketer, fr_last_id, recorder_on
 from .optim import CosineAnnealingLR, FusedSGD
 from .params import ParamStore
 from .utils import AverageMeter, Logger
@@ -46,6 +47,15 @@ def normalize_wave(w):
     zero-padded row, whole row included (no attention mask, Q13) — on the GPU (dfk_wave_normalize)."""
     from . import kernels as K
     return K.wave_normalize(w)
+
+
+def check_finite(loss, step):
+    """Failure detection at log steps (the only host sync of the loop): a NaN / Inf loss stops training with an
+    error instead of stepping SGD on garbage.  The attention kernels are built without NaN semantics
+    (build.py), so a diverging run is caught here, at the loss, not inside the kernels."""
+    if not math.isfinite(loss):
+        raise FloatingPointError(f"non-finite training loss {loss} at optimizer step {step}")
+    return loss
 
 
 def prepare_video(video, device, augment=False, generator=None):
@@ -203,29 +213,48 @@ class TrainStep:
         if self.bucketer.enabled and not recorder_on():   # the same environment on every rank: all go eager
             return None, RuntimeError("TORCH_FR_BUFFER_SIZE unset: the RCCL watchdog cannot be observed idle"), None
         for overlap, bn in forms:
-            self.bucketer.drain(self.bucketer.last_works)
-            g = torch.cuda.CUDAGraph()
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            self.bucketer.overlap = overlap
-            self.bucketer.reset()
-            self.store.uses.clear()   # a failed attempt may have left forward-use counts behind
-            ok, outs = True, None
+            # every failure below (drain timeout included) is local to this rank: it only marks the attempt
+            # failed, so every rank still reaches the _agree all-reduce and all move to the next form together
+            g, outs, ok = None, None, True
             try:
-                with torch.cuda.stream(s):
-                    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                        outs = body(overlap, bn)
-            except RuntimeError as e:         # e.g. a collective the backend cannot capture in this form
-                torch.cuda.synchronize()
+                self.bucketer.drain(self.bucketer.last_works)
+            except RuntimeError as e:
                 err, ok = e, False
-            torch.cuda.current_stream().wait_stream(s)
-            self.bucketer.overlap = True
-            self.bucketer.reset()
+            if ok:
+                fr0 = fr_last_id() if self.bucketer.watched() else None
+                self.bucketer.overlap = overlap
+                self.bucketer.reset()
+                self.store.uses.clear()   # a failed attempt may have left forward-use counts behind
+                try:
+                    g, outs = self._capture_once(body, overlap, bn)
+                except RuntimeError as e:     # e.g. a collective the backend cannot capture in this form
+                    err, ok, g = e, False, None
+                    if fr0 is not None:       # its captured collectives never run: the drain must not wait on them
+                        self.bucketer.fr_exclude.append((fr0, fr_last_id()))
+                self.bucketer.overlap = True
+                self.bucketer.reset()
             if not self._agree(ok):
                 del g
                 continue
             return g, outs, (overlap, bn)
         return None, err, None
+
+    def _capture_once(self, body, overlap, bn):
+        """One capture of body(overlap, bn) in thread-local mode on a side stream -> (graph, outputs); raises
+        RuntimeError when the capture fails (the device is synchronised first)."""
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        try:
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                    outs = body(overlap, bn)
+        except RuntimeError:
+            torch.cuda.synchronize()
+            torch.cuda.current_stream().wait_stream(s)
+            raise
+        torch.cuda.current_stream().wait_stream(s)
+        return g, outs
 
     def _step_body(self, static_in, static_label, accum):
         """The optimizer step's graph body: (zeroing,) BN broadcast, fwd + bwd, all-reduces, SGD."""
@@ -425,6 +454,7 @@ class Trainer:
                     self.scheduler.step()
                     if t % self.log_step == 0:
                         li = loss.item()
+                        check_finite(li, t)
                         stat.update(li)
                         dt = time.time() - t0
                         self.logger("| epoch {:2d} | step {:4d} | lr {:.4E} | Train Loss Avg {:3.5f} | clips/s {:.2f}"

@@ -280,3 +280,102 @@ def test_trainer_seeds_device_rng_per_rank():
     assert st[0][2] == st[1][2]
     rng.manual_seed(42, 1)
     assert rng.state("cpu").tolist()[0] == st[1][0]
+
+
+def _agree_worker(rank, world, port, fail, q):
+    """TrainStep._graph on CPU with the capture mechanics stubbed: `fail` names what breaks on rank 1 at the
+    first form ('capture': the capture body raises; 'drain': the pre-capture watchdog drain times out).  Every
+    rank must still reach _agree's MIN all-reduce and all must commit to the same (second) form."""
+    from deepfake_amd.trainer import TrainStep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCH_FR_BUFFER_SIZE="2000")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m = ProbNet()
+    store = ParamStore(m, torch.float32, device=torch.device("cpu"))
+    bk = GradBucketer(store, bucket_mb=0.0002)
+    step = TrainStep(m, store, _PlainSGD(store, 0.1), bk)
+    calls = []
+
+    def capture_once(body, overlap, bn):
+        calls.append((overlap, bn))
+        if fail == "capture" and rank == 1 and len(calls) == 1:
+            raise RuntimeError("stub: this form cannot be captured here")
+        return "graph", ("outs", overlap, bn)
+
+    real_drain = bk.drain
+    drains = []
+
+    def drain(works=(), timeout=60.0):
+        drains.append(1)
+        if fail == "drain" and rank == 1 and len(drains) == 1:
+            raise RuntimeError("stub: RCCL watchdog still tracks 1 collectives")
+        return real_drain(works, timeout)
+
+    step._capture_once = capture_once
+    bk.drain = drain
+    g, outs, form = step._graph(lambda o, b: None, TrainStep.FORMS)
+    q.put((rank, g, form, len(calls), bk.overlap))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", ["capture", "drain"])
+def test_capture_failure_on_one_rank_moves_all_ranks(fail):
+    """A rank whose capture (or pre-capture drain) fails alone does not diverge: all ranks drop the overlapped
+    form together and commit to the one-pass form (src/trainer.py:74-75 replaced by per-GPU DDP, §8e)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29531 if fail == "capture" else 29533
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, fail, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, form, n, ov)) for r, g, form, n, ov in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        g, form, n, ov = res[r]
+        assert g == "graph" and form == (False, True), (r, res[r])
+        assert ov is True      # the bucketer is left in its eager (hooked) state
+    assert res[0][2] == 2 and res[1][2] == (2 if fail == "capture" else 1)
+
+
+@pytest.mark.parametrize("world", [4])
+def test_bf16_buckets_world4(world):
+    """world 4, bf16 buckets over the real fused C1 layout: every rank's value is rounded to bf16 once and the
+    ring sums up to world-1 partials in bf16, so |got - mean| <= (2*world-1) * 2^-9 * mean(|v|) per element
+    (each rounding is at most 2^-9 of the magnitude it rounds)."""
+    from deepfake_amd.models.fused import build_fused
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_layout_worker, args=(r, world, 29541, torch.bfloat16, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, g) for r, g, _, _ in (q.get(timeout=300) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+    m = build_fused("c1")
+    store = ParamStore(m, torch.float32, device=torch.device("cpu"))
+    ref = torch.zeros_like(store.grad)
+    scale = torch.zeros_like(store.grad)
+    for rank in range(world):
+        for i, p in enumerate(store.params):
+            g = torch.Generator().manual_seed(1000 * rank + i)
+            s, e = store.span(i)
+            v = torch.randn(p.shape, generator=g).reshape(-1)
+            ref[s:e] += v / world
+            scale[s:e] += v.abs() / world
+    bound = (2 * world - 1) * 2.0 ** -9
+    for r in range(world):
+        got = torch.from_numpy(res[r])
+        assert bool(((got - ref).abs() <= bound * scale + 1e-6).all()), float(((got - ref).abs() / (scale + 1e-6)).max())
+        assert torch.equal(got, torch.from_numpy(res[0]))
+
+
+def test_watchdog_idle_raises_without_flight_recorder(monkeypatch):
+    """No flight-recorder dump in this torch build: the drain must raise, not return at once (an empty entry
+    list would otherwise read as 'watchdog idle' and the capture abort race would come back silently)."""
+    from torch._C import _distributed_c10d as c10d
+    from deepfake_amd import ddp
+    for n in ("_dump_nccl_trace_json", "_dump_fr_trace_json"):
+        monkeypatch.delattr(c10d, n, raising=False)
+    with pytest.raises(RuntimeError, match="flight-recorder"):
+        ddp.watchdog_idle(timeout=0.1)

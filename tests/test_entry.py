@@ -104,3 +104,14 @@ def test_processor_padding_longest():
     over the whole padded row, Q13)."""
     w = pad_longest([np.ones(3, np.float32), np.arange(5, dtype=np.float32)])
     assert w.shape == (2, 5) and w[0].tolist() == [1, 1, 1, 0, 0] and w[1].tolist() == [0, 1, 2, 3, 4]
+
+
+def test_check_finite_stops_on_nan_loss():
+    """Failure detection at log steps: a NaN / Inf loss raises instead of being logged and stepped on."""
+    import math
+    import pytest
+    from deepfake_amd.trainer import check_finite
+    assert check_finite(0.69, 1) == 0.69
+    for bad in (math.nan, math.inf, -math.inf):
+        with pytest.raises(FloatingPointError):
+            check_finite(bad, 3)
