@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--deterministic", action="store_true", help="regularisers off (the parity setting)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=3)
+    p.add_argument("--cpu-threads", type=int, default=None, help="torch threads of the CPU baseline (default: every "
+                   "CPU in this process's affinity mask within its cgroup CPU quota, BASELINE.md §4)")
     p.add_argument("--roofline-iters", type=int, default=20)
     return p.parse_args()
 
@@ -90,31 +92,43 @@ ROOFLINE_KERNEL = "wattn_fwd3_kernel<32, true, false>"
 ROOFLINE_PMC = os.path.join(HERE, "profiles", "r3o_wattn_fwd_pmc.json")
 
 
+def stage1_geometry(cfg):
+    """Stage-1 attention geometry of this config's video trunk: (C, heads, window, shift, (D, H, W))."""
+    v = cfg["vst"]
+    C, heads = v["embed_dim"], v["num_heads"][0]
+    dims = (cfg["T"] // 2, cfg["H"] // 4, cfg["W"] // 4)
+    win = tuple(min(w, d) for w, d in zip(v["window_size"], dims))
+    shift = tuple(0 if d <= w else w // 2 for w, d in zip(v["window_size"], dims))
+    return C, heads, win, shift, dims
+
+
 def roofline_case(cfg, B, dt):
-    """Dominant MFMA kernel: the stage-1 shifted-window attention core of the Swin-T
-    video backbone at this workload (B clips; window 8x7x7 = 392 tokens, 3 heads x 32,
-    shift (4,3,3), relative-position bias).  Returns (launch fn, algorithmic FLOPs per
-    launch = 4 * windows * heads * N^2 * hd, i.e. QK^T and PV)."""
+    """Dominant MFMA kernel: the stage-1 shifted-window attention core of this config's video backbone
+    (B clips; Swin-T / Swin-B: window 8x7x7 = 392 tokens, 3 / 4 heads x 32, shift (4,3,3), relative-position
+    bias).  Returns (launch fn, algorithmic FLOPs per launch = 4 * windows * heads * N^2 * hd, i.e. QK^T and
+    PV, description)."""
     from deepfake_amd import kernels as K
-    D, H, W = cfg["T"] // 2, cfg["H"] // 4, cfg["W"] // 4
-    heads, hd, C = 3, 32, 96
+    C, heads, win, shift, (D, H, W) = stage1_geometry(cfg)
+    hd = C // heads
     rows = B * D * H * W
     g = torch.Generator(device="cuda").manual_seed(7)
     qkv = torch.randn(rows, 3 * C, device="cuda", generator=g).to(dt)
-    win = (8, 7, 7)
-    nW = (D // 8) * (H // 7) * (W // 7)
-    N = 392
+    nW = -(-D // win[0]) * -(-H // win[1]) * -(-W // win[2])
+    N = win[0] * win[1] * win[2]
     flops = 4.0 * B * nW * heads * N * N * hd
-    rpb = torch.randn(15 * 13 * 13, heads, device="cuda", generator=g) * 0.02
+    L = (2 * win[0] - 1) * (2 * win[1] - 1) * (2 * win[2] - 1)
+    rpb = torch.randn(L, heads, device="cuda", generator=g) * 0.02
     out = torch.empty(rows, C, device="cuda", dtype=dt)
-    args = (qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, (B, D, H, W), win, win, (4, 3, 3), heads, hd, hd ** -0.5)
+    args = (qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, (B, D, H, W), win, win, shift, heads, hd, hd ** -0.5)
     # the bf16 score-bias tiles (dfk_wattn_table, a separate launch) are built once: the timed launch is the
     # attention kernel alone, the one rocprofv3 lists as wattn_fwd3_kernel<32, true, false>
     _, _, tab = K.wattn_fwd(*args, rpb=rpb, out=out, return_table=True)
 
     def run():
         K.wattn_fwd(*args, rpb=rpb, out=out, need_lse=True, tab=tab)
-    return run, flops
+    desc = (f"stage-1 SW-MSA core, {N}-token windows, {heads} heads x {hd}, shift {'x'.join(map(str, shift))}, RPB, "
+            f"{B * nW * heads} window-heads")
+    return run, flops, desc
 
 
 def pmc_traffic():
@@ -146,7 +160,7 @@ def conv3d_in_step():
         return None
 
 
-def conv3d_roofline(cfg, B, iters, nbuf=3):
+def conv3d_roofline(cfg, B, iters, nbuf=3, instep=False):
     """The whole Conv3D patch embed (PatchEmbed3D pad + Conv3d(3->96, 2x4x4) + LayerNorm(96),
     video_swin_transformer.py:446-458) as the ONE fused launch the training step runs
     (dfk_patch_embed_fwd): the fp32 clip batch [B,T,3,H,W] is read once, the normalised bf16 tokens
@@ -157,7 +171,7 @@ def conv3d_roofline(cfg, B, iters, nbuf=3):
     from deepfake_amd import kernels as K
     g = torch.Generator(device="cuda").manual_seed(5)
     vids = [torch.randn(B, cfg["T"], 3, cfg["H"], cfg["W"], device="cuda", generator=g) for _ in range(nbuf)]
-    C = 96
+    C = cfg["vst"]["embed_dim"]
     w = (torch.randn(C, 96, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
     b, lw, lb = (torch.randn(C, device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
     tokens = B * (cfg["T"] // 2) * (cfg["H"] // 4) * (cfg["W"] // 4)
@@ -169,19 +183,19 @@ def conv3d_roofline(cfg, B, iters, nbuf=3):
         K.patch_embed_fwd(vids[state["i"]], "btchw", w, b, lw, lb, 1e-5)
     t = time_kernel(run, iters)
     achieved = nbytes / t / 1e9
-    return {"kernel": CONV3D_KERNEL + " (fused pad + Conv3d 2x4x4 + LayerNorm of the clip batch, cold)",
+    return {"kernel": CONV3D_KERNEL + f" (fused pad + Conv3d 2x4x4 -> {C} + LayerNorm of the clip batch, cold)",
             "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4), "bytes_per_launch": nbytes, "avg_launch_ms": round(t * 1e3, 4),
             "timing": f"HIP events over {iters} launches rotating {nbuf} clip batches (working set > Infinity Cache)",
-            "in_step": conv3d_in_step() if cfg["T"] == 32 and B == 8 else None}
+            "in_step": conv3d_in_step() if instep else None}
 
 
-def roofline(cfg, B, dt, iters):
-    run, flops = roofline_case(cfg, B, dt)
+def roofline(cfg, B, dt, iters, pmc=True):
+    run, flops, desc = roofline_case(cfg, B, dt)
     t = time_kernel(run, iters)
     achieved = flops / t / 1e12
-    traffic, src = pmc_traffic()
-    return {"kernel": ROOFLINE_KERNEL + " (stage-1 SW-MSA core, 392-token windows, shift 4x3x3, RPB)",
+    traffic, src = pmc_traffic() if pmc else (None, None)
+    return {"kernel": ROOFLINE_KERNEL + f" ({desc})",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
             "traffic_source": src, "flops_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4)}
@@ -191,14 +205,16 @@ GEMM_KERNEL = "gemm_dma_kernel<32|64, N, N, 2>"
 
 
 def gemm_roofline(cfg, B, iters):
-    """The step's largest Linear by time on the MFMA path: Swin-T stage-3 Mlp.fc1 forward
+    """The step's largest Linear by time on the MFMA path: the video trunk's stage-3 Mlp.fc1 forward
     (video_swin_transformer.py Mlp, src/utils.py:254-256) with its fused bias + GELU epilogue that also
-    saves the pre-activation — tokens = B * (T/2) * (H/16) * (W/16) rows, 384 -> 1536.  Algorithmic FLOPs
-    per launch = 2 * M * N * K (the epilogue's elementwise work is not counted)."""
+    saves the pre-activation — tokens = B * (T/2) * (H/16) * (W/16) rows, 4C -> 16C (Swin-T 384 -> 1536,
+    Swin-B 512 -> 2048).  Algorithmic FLOPs per launch = 2 * M * N * K (the epilogue's elementwise work is
+    not counted)."""
     from deepfake_amd import kernels as K
     g = torch.Generator(device="cuda").manual_seed(9)
     M = B * (cfg["T"] // 2) * (cfg["H"] // 16) * (cfg["W"] // 16)
-    Kd, N = 384, 1536
+    Kd = 4 * cfg["vst"]["embed_dim"]
+    N = 4 * Kd
     x = torch.randn(M, Kd, device="cuda", generator=g).to(torch.bfloat16)
     w = (torch.randn(N, Kd, device="cuda", generator=g) * Kd ** -0.5).to(torch.bfloat16)
     b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
@@ -210,7 +226,8 @@ def gemm_roofline(cfg, B, iters):
     t = time_kernel(run, iters)
     flops = 2.0 * M * N * Kd
     achieved = flops / t / 1e12
-    return {"kernel": GEMM_KERNEL + f" (Swin-T stage-3 Mlp.fc1 fwd, [{M},{Kd}]x[{Kd},{N}] + bias + GELU, pre-activation saved)",
+    trunk = "Swin-B" if cfg["vst"]["embed_dim"] == 128 else "Swin-T"
+    return {"kernel": GEMM_KERNEL + f" ({trunk} stage-3 Mlp.fc1 fwd, [{M},{Kd}]x[{Kd},{N}] + bias + GELU, pre-activation saved)",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "flops_per_launch": flops,
             "bytes_per_launch": (M * Kd + 2 * M * N + N * Kd) * 2, "avg_launch_ms": round(t * 1e3, 4)}
@@ -239,12 +256,31 @@ def _cpu_train_rate(cfg_name, B, steps):
     return statistics.median(times)
 
 
-def cpu_baseline(cfg_name, steps):
+def usable_cpus():
+    """CPUs this process may actually use: its affinity mask, capped by the cgroup CPU quota (cpu.max) and by
+    OMP_NUM_THREADS when the launcher sets it.  On the
+    GPU box the mask lists 256 CPUs but the quota is 16 per GPU: the C2 oracle step took 5.7 s at 16 torch
+    threads, 10.4 s at 64 and did not finish in 180 s at 256 (profiles/fp8/r4_mx_lane_map_probe.txt)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, math.ceil(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")   # the job's thread budget, when its launcher states one
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
+def cpu_baseline(cfg_name, steps, threads=None):
     """the oracle (CPU restatement of the reference, pinned to the reference's golden
     vectors) timed on the host cores: C1 and C2 at B=2, train-mode BatchNorm, one warm-up step then the
     median of `steps` train steps.  value = the C2 rate (the metric's workload)."""
     cores = len(os.sched_getaffinity(0))   # host CPUs this process may run on
-    threads = min(cores, 16)                # the GPU box's CPU share per GPU is 16
+    threads = usable_cpus() if threads is None else threads   # BASELINE.md §4: every CPU this process may use
     torch.set_num_threads(threads)
     cpu_model = "unknown"
     try:
@@ -258,8 +294,8 @@ def cpu_baseline(cfg_name, steps):
             "affinity_cpus": cores, "kind": "port",
             "c1_clips_per_s": round(2.0 / t1, 3), "cpu_model": cpu_model,
             "sample": f"oracle fp32 CPU train step (train-mode BN) at B=2: {cfg_name.upper()} {t2:.2f} s/step, "
-                      f"C1 {t1:.3f} s/step; median of {steps} steps after 1 warm-up, {threads} torch threads on "
-                      f"{cores} affinity CPUs"}
+                      f"C1 {t1:.3f} s/step; median of {steps} steps after 1 warm-up, {threads} torch threads = the CPUs "
+                      f"usable under the cgroup quota ({cores} in the affinity mask)"}
 
 
 def workload_name(name, cfg):
@@ -324,13 +360,15 @@ def main():
     clips = world * a.batch * a.steps
     value = clips / el
 
-    roof = roofline(cfg, a.batch, dt, a.roofline_iters) if rank == 0 else None
-    roof_conv = conv3d_roofline(cfg, a.batch, a.roofline_iters) if rank == 0 else None
+    # committed counter / trace files describe the C2 bench command only: other configs report none
+    c2 = a.config == "c2" and a.batch == 8
+    roof = roofline(cfg, a.batch, dt, a.roofline_iters, pmc=c2) if rank == 0 else None
+    roof_conv = conv3d_roofline(cfg, a.batch, a.roofline_iters, instep=c2) if rank == 0 else None
     roof_gemm = gemm_roofline(cfg, a.batch, a.roofline_iters) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(a.config, a.cpu_steps)
+            cpu = cpu_baseline(a.config, a.cpu_steps, a.cpu_threads)
         except Exception as e:  # noqa: BLE001 — the baseline must not hide the measured line
             cpu = {"value": None, "unit": "clips/s", "cores": None, "kind": "port", "sample": f"failed: {e!r}"}
     if rank == 0:

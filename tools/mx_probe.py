@@ -33,15 +33,23 @@ def cd(shape, D):
     return out
 
 
+def kmap(shape, g, j):
+    """Decoded operand map: byte j of lane group g (= lane // M) holds k = KH*(j >> 4) + 16 g + (j & 15), i.e. two
+    16-byte halves, half h covering k in [KH h + 16 g, +16) with KH = 64 (16x16x128) or 32 (32x32x64)."""
+    return (64 if shape == 16 else 32) * (j >> 4) + 16 * g + (j & 15)
+
+
 def model(shape, a, b, sa, sb):
-    """The decoded model: lane l holds A[row l%M][k = 32 (l // M) + j] (B: col), scale byte 0 of lane l scales
-    those 32 products."""
+    """The decoded model: lane l holds A[row l%M][k = kmap(l // M, j)] in byte j (B: col); byte 0 of lane
+    (i + M kb)'s scale VGPR is the E8M0 scale of row (col) i's k-block kb = k >> 5."""
     M = 16 if shape == 16 else 32
     fa = np.exp2((sa & 0xff).astype(np.float64) - 127)
     fb = np.exp2((sb & 0xff).astype(np.float64) - 127)
     R = np.zeros((M, M))
     for g in range(64 // M):
-        R += (a[g * M:(g + 1) * M] * fa[g * M:(g + 1) * M, None]) @ (b[g * M:(g + 1) * M] * fb[g * M:(g + 1) * M, None]).T
+        for j in range(32):
+            kb = kmap(shape, g, j) >> 5
+            R += np.outer(a[g * M:(g + 1) * M, j] * fa[kb * M:(kb + 1) * M], b[g * M:(g + 1) * M, j] * fb[kb * M:(kb + 1) * M])
     return R
 
 
@@ -82,7 +90,7 @@ def main(path):
             ref = model(shape, e4m3(A[e].reshape(-1)).reshape(64, 32), e4m3(B[e].reshape(-1)).reshape(64, 32),
                         SA[e], SB[e])
             err = np.abs(got - ref).max()
-            print(f"  model check ({'A' if e == 384 else 'B'} scales random): max |err| {err:.4g} of {np.abs(ref).max():.4g}")
+            print(f"  model check ({'A' if e == 384 else 'B'} scales random, decoded map): max |err| {err:.4g} of {np.abs(ref).max():.4g}")
             ok &= err == 0
     n = 1 << 16
     x = np.frombuffer(raw, np.float32, n, o); o += 4 * n
