@@ -54,7 +54,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c2")
     p.add_argument("--batch", type=int, default=8)
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                   help="fp8: bf16 compute with the video trunk's stage-3/4 Linears on MX-fp8 GEMMs (C4's fp8 path)")
     p.add_argument("--eager", action="store_true", help="run the step eagerly instead of replaying its HIP graph")
     p.add_argument("--deterministic", action="store_true", help="regularisers off (the parity setting)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -204,7 +205,11 @@ def roofline(cfg, B, dt, iters, pmc=True):
 GEMM_KERNEL = "gemm_dma_kernel<32|64, N, N, 2>"
 
 
-def gemm_roofline(cfg, B, iters):
+PEAK_FP8_TFLOPS = 5000.0       # MI355X dense fp8 (block-scaled MX e4m3) MFMA (MI355X_MICROARCH.md)
+MX_GEMM_KERNEL = "gemm_mx_kernel<64, 2, 2, 2, true>"
+
+
+def gemm_roofline(cfg, B, iters, fp8=False):
     """The step's largest Linear by time on the MFMA path: the video trunk's stage-3 Mlp.fc1 forward
     (video_swin_transformer.py Mlp, src/utils.py:254-256) with its fused bias + GELU epilogue that also
     saves the pre-activation — tokens = B * (T/2) * (H/16) * (W/16) rows, 4C -> 16C (Swin-T 384 -> 1536,
@@ -220,13 +225,26 @@ def gemm_roofline(cfg, B, iters):
     b = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     aux = torch.empty_like(out)
+    trunk = "Swin-B" if cfg["vst"]["embed_dim"] == 128 else "Swin-T"
+    flops = 2.0 * M * N * Kd
+    if fp8:   # the step's MX-fp8 fc1: e4m3 operands with E8M0 block scales, GELU epilogue + MX copy of h for fc2
+        xq, wq = K.mx_quant(x), K.mx_quant(w.float())
+
+        def run_mx():
+            K.gemm_mx(xq, wq, bias=b, out=out, act=1, aux=aux, mx_out=True)
+        t = time_kernel(run_mx, iters)
+        achieved = flops / t / 1e12
+        return {"kernel": MX_GEMM_KERNEL + f" ({trunk} stage-3 Mlp.fc1 fwd on MX-fp8, [{M},{Kd}]x[{Kd},{N}] + bias + "
+                "GELU, pre-activation saved, h also written quantised for fc2)",
+                "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP8_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_FP8_TFLOPS, 4), "flops_per_launch": flops,
+                "bytes_per_launch": M * Kd * (1 + 1 / 32) + N * Kd * (1 + 1 / 32) + M * N * (2 + 2 + 1 + 1 / 32),
+                "avg_launch_ms": round(t * 1e3, 4)}
 
     def run():
         K.linear(x, w, b, out=out, act=1, aux=aux)
     t = time_kernel(run, iters)
-    flops = 2.0 * M * N * Kd
     achieved = flops / t / 1e12
-    trunk = "Swin-B" if cfg["vst"]["embed_dim"] == 128 else "Swin-T"
     return {"kernel": GEMM_KERNEL + f" ({trunk} stage-3 Mlp.fc1 fwd, [{M},{Kd}]x[{Kd},{N}] + bias + GELU, pre-activation saved)",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "flops_per_launch": flops,
@@ -315,7 +333,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
-    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    dt = torch.float32 if a.dtype == "fp32" else torch.bfloat16
 
     from deepfake_amd.ddp import GradBucketer
     from deepfake_amd.models.fused import CONFIGS, build_fused
@@ -327,7 +345,7 @@ def main():
     cfg = CONFIGS[a.config]
     torch.manual_seed(1234)
     rng.manual_seed(1234, rank)
-    model = build_fused(cfg, compute_dtype=dt, regularize=not a.deterministic).to(device)
+    model = build_fused(cfg, compute_dtype=dt, regularize=not a.deterministic, fp8=a.dtype == "fp8").to(device)
     model.train()
     store = ParamStore(model, dt)
     bucketer = GradBucketer(store, bucket_mb=64.0)
@@ -364,7 +382,7 @@ def main():
     c2 = a.config == "c2" and a.batch == 8
     roof = roofline(cfg, a.batch, dt, a.roofline_iters, pmc=c2) if rank == 0 else None
     roof_conv = conv3d_roofline(cfg, a.batch, a.roofline_iters, instep=c2) if rank == 0 else None
-    roof_gemm = gemm_roofline(cfg, a.batch, a.roofline_iters) if rank == 0 else None
+    roof_gemm = gemm_roofline(cfg, a.batch, a.roofline_iters, fp8=a.dtype == "fp8") if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:

@@ -35,7 +35,12 @@ class GemmArgs(C.Structure):
                 ("a_kmajor", C.c_int32), ("b_kmajor", C.c_int32), ("c_f32", C.c_int32), ("nz0", C.c_int32),
                 ("nz1", C.c_int32), ("splitk", C.c_int32), ("act", C.c_int32), ("atomic", C.c_int32),
                 ("beta", C.c_float), ("ws", C.c_void_p), ("rowsum", C.c_void_p), ("drop", Drop),
-                ("alpha", C.c_float)]
+                ("alpha", C.c_float), ("mx_q", C.c_void_p), ("mx_s", C.c_void_p), ("mx_ldq", C.c_int64),
+                ("mx_lds", C.c_int64)]
+
+
+class MxOperand(C.Structure):
+    _fields_ = [("q", C.c_void_p), ("s", C.c_void_p), ("ld", C.c_int64), ("lds", C.c_int64)]
 
 
 class WattnArgs(C.Structure):
@@ -84,6 +89,8 @@ SIGNATURES = {
     "dfk_gemm": [C.POINTER(GemmArgs), _VP],
     "dfk_gemm_workspace": [C.POINTER(GemmArgs)],
     "dfk_colsum": [_VP, C.c_int, _I64, _I64, _I64, _VP, _VP],
+    "dfk_gemm_mx": [C.POINTER(GemmArgs), C.POINTER(MxOperand), C.POINTER(MxOperand), _VP],
+    "dfk_mx_quant": [_VP, C.c_int, _I64, _I64, _I64, C.c_int, _VP, _I64, _VP, _VP],
     "dfk_layernorm_fwd": [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, _F, C.c_int, _VP, C.POINTER(Drop), _VP],
     "dfk_layernorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, C.c_int, C.c_int, _VP,
                           C.POINTER(Drop), _VP],

@@ -233,10 +233,12 @@ __device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1
   }
 }
 
-template <typename T, int WT>
+template <typename T, int WT, bool MXO = false>
 __device__ __forceinline__ void tile_epilogue(const dfk_gemm_args& g, float* smem, const f32x4 (&acc)[WT / 16][WT / 16],
                                               int lane, int wave, int wm, int wn, int bm, int bn, int z, int split,
                                               int evec, float* slab);
+__device__ __forceinline__ int mx_scale_byte(float am);
+__device__ __forceinline__ uint2 mx_pack8(const float (&v)[8], int e);
 
 template <typename T, int WT, bool AK, bool BKM, bool VECOK, bool CONV, bool RS = false>
 __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int evec, float* slab) {
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
 // Epilogue shared by the GEMM kernels: stage each wave's WT x WT fp32 tile through LDS (the 16x16 MFMA C/D
 // layout is col = lane&15, row = (lane>>4)*4 + r), then every lane owns 8 consecutive columns of a row:
 // 16-B loads of bias/residual/aux and 16-B stores.  The caller has passed a barrier after its last LDS read.
-template <typename T, int WT>
+template <typename T, int WT, bool MXO>
 __device__ __forceinline__ void tile_epilogue(const dfk_gemm_args& g, float* smem, const f32x4 (&acc)[WT / 16][WT / 16],
                                               int lane, int wave, int wm, int wn, int bm, int bn, int z, int split,
                                               int evec, float* slab) {
@@ -433,11 +435,35 @@ __device__ __forceinline__ void tile_epilogue(const dfk_gemm_args& g, float* sme
   for (int pass = 0; pass < WT / RPP; ++pass) {
     const int rl = pass * RPP + lane / CPR;
     const int row = bm + wm * WT + rl;
-    if (row >= g.M || col0 >= g.N) continue;
-    float v[8];
-    *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(es + rl * ES + c8);
-    *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(es + rl * ES + c8 + 4);
-    epilogue8<T>(g, z0, z1, row, col0, v, evec);
+    if constexpr (MXO) {
+      // MX copy of the stored bf16 C along N: lanes 4q..4q+3 hold the 32 columns of one block of this row
+      const bool ok = row < g.M && col0 < g.N;
+      float v[8];
+      *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(es + rl * ES + c8);
+      *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(es + rl * ES + c8 + 4);
+      if (ok) epilogue8<T>(g, z0, z1, row, col0, v, evec);
+      float am = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = ok ? bf2f(f2bf(v[e])) : 0.f;
+        am = fmaxf(am, fabsf(v[e]));
+      }
+      am = fmaxf(am, __shfl_xor(am, 1, 64));
+      am = fmaxf(am, __shfl_xor(am, 2, 64));
+      const int eb = mx_scale_byte(am);
+      const uint2 w = mx_pack8(v, eb);
+      if (ok) {
+        *reinterpret_cast<uint2*>(g.mx_q + (long)row * g.mx_ldq + col0) = w;
+        if ((lane & 3) == 0)
+          reinterpret_cast<uint8_t*>(g.mx_s)[((long)(col0 >> 7) * g.mx_lds + row) * 4 + ((col0 & 127) >> 5)] = (uint8_t)eb;
+      }
+    } else {
+      if (row >= g.M || col0 >= g.N) continue;
+      float v[8];
+      *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(es + rl * ES + c8);
+      *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(es + rl * ES + c8 + 4);
+      epilogue8<T>(g, z0, z1, row, col0, v, evec);
+    }
   }
 }
 
@@ -880,10 +906,240 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   return 0;
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// MX-fp8 GEMM (include/dfk.h dfk_gemm_mx): C = A B^T with A [M][K], B [N][K] OCP e4m3 + E8M0 block scales, on
+// v_mfma_scale_f32_16x16x128_f8f6f4 — one MFMA covers a whole 128-k tile, at twice the bf16 rate per clock.
+// Lane map of that instruction, decoded on the hardware (tools/mx_probe.hip, profiles/fp8/r4_mx_lane_map_probe.txt):
+// lane l holds row (col) l&15 of A (B); its 32 bytes are two 16-byte halves, half h = k [64h + 16(l>>4), +16); the
+// E8M0 scale of row i's k-block kb (k in [32kb, 32kb+32)) is byte 0 of lane (i + 16kb)'s scale VGPR.  So a k-tile
+// image [ROWS][128 B] is the bf16 kernel's [ROWS][64 bf16] image byte for byte: same source-side XOR swizzle, and
+// the two 16-B fragment reads of lane l are chunks (l>>4) and 4 + (l>>4) of its row (conflict-free, as the bf16
+// kernel's k-steps 0 and 1).  Scales: per k-tile one dword per row (the 4 block scales), DMA'd 4 B per lane into a
+// per-stage scale image; lane l shifts its row's dword right by 8(l>>4) (the instruction reads byte 0 only).
+// The accumulator must stay loop-carried (dst tied to srcC): with a fresh zero C, hipcc once placed the destination
+// over srcA and the hardware result was wrong (r4a probe).
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+template <int ROWS, int NWV>
+struct Dma8 {   // one operand's [ROWS][128 B] k-tile image: chunk c of row r stored at c ^ ((r>>1)&7)
+  static constexpr int NI = ROWS / (8 * NWV);
+  __device__ static __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, uint32_t ld, int row0, int rowlim, int k0,
+                                               uint8_t* img, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int sl = (wave * NI + i) * 64 + lane;
+      const int r = sl >> 3, c = (sl & 7) ^ ((r >> 1) & 7);
+      const int vr = row0 + r;
+      const uint32_t off = (uint32_t)vr * ld + (uint32_t)(k0 + c * 16);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + (wave * NI + i) * 1024), 16,
+                                               vr < rowlim ? off : 0x80000000u, 0, 0, 0);
+    }
+  }
+};
+
+__device__ __forceinline__ i32x8 frag_mx(const uint8_t* img, int r0, int lane) {
+  const int r = r0 + (lane & 15), g = lane >> 4, sw = (r >> 1) & 7;
+  const uint4 lo = *reinterpret_cast<const uint4*>(img + r * 128 + ((g ^ sw) << 4));
+  const uint4 hi = *reinterpret_cast<const uint4*>(img + r * 128 + (((4 + g) ^ sw) << 4));
+  return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
+template <int WT, int NWM, int NWN, int S, bool MXO>
+__global__ __launch_bounds__(NWM * NWN * 64) void gemm_mx_kernel(const dfk_gemm_args g, const dfk_mx_operand ma,
+                                                                 const dfk_mx_operand mb, int evec) {
+  constexpr int NWV = NWM * NWN, BM = NWM * WT, BN = NWN * WT, MI = WT / 16, BK = 128;
+  constexpr int RW = (BM + BN) / NWV;                 // scale rows DMA'd per wave (one 4-B-per-lane instruction)
+  static_assert(RW <= 64 && BM % RW == 0, "scale DMA split");
+  constexpr int STAGE = (BM + BN) * BK + NWV * 256;   // operand images + per-wave 256-B scale slots (bytes)
+  constexpr int ES = WT + 4;
+  constexpr int SMEM = S * STAGE > NWV * WT * ES * 4 ? S * STAGE : NWV * WT * ES * 4;
+  constexpr int LPT = Dma8<BM, NWV>::NI + Dma8<BN, NWV>::NI + 1;   // DMA instructions per wave per k-tile
+  __shared__ __attribute__((aligned(16))) float smem_f[SMEM / 4];   // the one LDS object (staging + epilogue)
+  uint8_t* smem = reinterpret_cast<uint8_t*>(smem_f);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / NWN, wn = wave % NWN;
+  int tn, tmi;
+  {
+    const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    const int nid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    tn = nid % gridDim.x;
+    tmi = nid / gridDim.x;
+  }
+  const int bn = tn * BN, bm = tmi * BM;
+  const int ntile = g.K / BK;
+  const uint32_t lda = (uint32_t)ma.ld, ldb = (uint32_t)mb.ld;
+  const __amdgpu_buffer_rsrc_t rqa = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(ma.q), (short)0, (int)((long)(g.M - 1) * ma.ld + g.K), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rqb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(mb.q), (short)0, (int)((long)(g.N - 1) * mb.ld + g.K), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(ma.s), (short)0, (int)(((long)(ntile - 1) * ma.lds + g.M) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(mb.s), (short)0, (int)(((long)(ntile - 1) * mb.lds + g.N) * 4), 0x00020000);
+  // this wave's scale rows: entries [wave*RW, wave*RW + RW) of (A tile rows ++ B tile rows) — all of one operand
+  const bool sc_a = wave * RW < BM;
+  const int sc_row = (sc_a ? bm + wave * RW : bn + wave * RW - BM) + lane;
+  const bool sc_in = lane < RW && sc_row < (sc_a ? g.M : g.N);
+  const uint32_t sc_ld = (uint32_t)(sc_a ? ma.lds : mb.lds);
+
+  auto issue = [&](int t, uint8_t* st) {
+    Dma8<BM, NWV>::issue(rqa, lda, bm, g.M, t * BK, st, wave, lane);
+    Dma8<BN, NWV>::issue(rqb, ldb, bn, g.N, t * BK, st + BM * BK, wave, lane);
+    const uint32_t off = ((uint32_t)t * sc_ld + (uint32_t)sc_row) * 4u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(sc_a ? rsa : rsb, (lds_void*)(st + (BM + BN) * BK + wave * 256), 4,
+                                             sc_in ? off : 0x80000000u, 0, 0, 0);
+  };
+
+  f32x4 acc[MI][MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int d = 0; d < S - 1; ++d)
+    if (d < ntile) issue(d, smem + d * STAGE);
+  for (int t = 0; t < ntile; ++t) {
+    if constexpr (S == 3) {
+      if (t + 1 < ntile) wait_vm<LPT>(); else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + S - 1 < ntile) issue(t + S - 1, smem + ((t + S - 1) % S) * STAGE);
+    const uint8_t* As = smem + (t % S) * STAGE;
+    const uint8_t* Bs = As + BM * BK;
+    const uint32_t* Ss = reinterpret_cast<const uint32_t*>(As + (BM + BN) * BK);
+    i32x8 af[MI], bfr[MI];
+    int sa[MI], sb[MI];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      af[mi] = frag_mx(As, wm * WT + mi * 16, lane);
+      const int i = wm * WT + mi * 16 + (lane & 15);
+      sa[mi] = (int)(Ss[(i / RW) * 64 + i % RW] >> (8 * (lane >> 4)));
+    }
+#pragma unroll
+    for (int ni = 0; ni < MI; ++ni) {
+      bfr[ni] = frag_mx(Bs, wn * WT + ni * 16, lane);
+      const int i = BM + wn * WT + ni * 16 + (lane & 15);
+      sb[ni] = (int)(Ss[(i / RW) * 64 + i % RW] >> (8 * (lane >> 4)));
+    }
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MI; ++ni)
+        acc[mi][ni] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0, sa[mi],
+                                                                        0, sb[ni]);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  tile_epilogue<bf16raw, WT, MXO>(g, smem_f, acc, lane, wave, wm, wn, bm, bn, 0, 0, evec, nullptr);
+}
+
+// ---- MX quantisation (dfk_mx_quant) ----
+// E8M0 scale byte of a 32-element block with max |x| = am: the smallest e with am / 2^(e-127) <= 448
+// (am = 1.m * 2^(E-127): e = E - 8, or E - 7 when 1.m > 1.75), clamped so 2^(127-e) is a normal float
+__device__ __forceinline__ int mx_scale_byte(float am) {
+  const uint32_t b = __float_as_uint(am);
+  int e = (int)((b >> 23) & 0xff) - 8 + ((b & 0x7fffffu) > 0x600000u ? 1 : 0);
+  e = am == 0.f ? 127 : e;
+  return min(max(e, 1), 253);
+}
+// 8 values -> 8 e4m3 bytes (x * 2^(127-e), rounded to nearest even)
+__device__ __forceinline__ uint2 mx_pack8(const float (&v)[8], int e) {
+  const float inv = __uint_as_float((uint32_t)(254 - e) << 23);
+  int w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, 0, false);
+  w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, w0, true);
+  int w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, 0, false);
+  w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, w1, true);
+  return make_uint2((uint32_t)w0, (uint32_t)w1);
+}
+// the 4 block scales of a 16-lane k-tile group -> one dword (valid in the group's first lane)
+__device__ __forceinline__ uint32_t mx_gather_scales(int e, int lane) {
+  const int base = lane & ~15;
+  const uint32_t b0 = (uint32_t)__shfl(e, base, 64), b1 = (uint32_t)__shfl(e, base + 4, 64);
+  const uint32_t b2 = (uint32_t)__shfl(e, base + 8, 64), b3 = (uint32_t)__shfl(e, base + 12, 64);
+  return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+}
+
+// along the rows' contiguous dim: one thread per 8 elements, 4 lanes per 32-block, 16 lanes per 128-k tile
+template <typename T>
+__global__ __launch_bounds__(256) void mx_quant_kernel(const T* __restrict__ x, long rows, int cols, long ldx,
+                                                       uint8_t* __restrict__ q, long ldq, uint32_t* __restrict__ s) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int cpr = cols >> 3;
+  const long r = t / cpr;
+  const int c8 = (int)(t - r * cpr);
+  const bool ok = r < rows;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (ok) ld8<T>(x + r * ldx + c8 * 8, v);
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(v[i]));
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  const int e = mx_scale_byte(am);
+  const uint2 w = mx_pack8(v, e);
+  const uint32_t sd = mx_gather_scales(e, lane);
+  if (ok) {
+    *reinterpret_cast<uint2*>(q + r * ldq + c8 * 8) = w;
+    if ((c8 & 15) == 0) s[(long)(c8 >> 4) * rows + r] = sd;
+  }
+}
+
+// x^T along x's rows: a 128 (r) x 64 (c) tile through LDS; output row c = 16 lanes x 8 consecutive r
+template <typename T>
+__global__ __launch_bounds__(256) void mx_quant_t_kernel(const T* __restrict__ x, int R, int C, long ldx,
+                                                         uint8_t* __restrict__ q, long ldq, uint32_t* __restrict__ s) {
+  __shared__ float tile[128][65];
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 128, tid = threadIdx.x, lane = tid & 63;
+#pragma unroll 4
+  for (int i = tid; i < 128 * 64; i += 256) {
+    const int rr = i >> 6, cc = i & 63;
+    tile[rr][cc] = c0 + cc < C ? ldf<T>(x + (long)(r0 + rr) * ldx + c0 + cc) : 0.f;
+  }
+  __syncthreads();
+  const int ch = tid & 15;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int cc = (tid >> 4) + 16 * it, c = c0 + cc;
+    float v[8];
+    float am = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      v[i] = tile[ch * 8 + i][cc];
+      am = fmaxf(am, fabsf(v[i]));
+    }
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    am = fmaxf(am, __shfl_xor(am, 2, 64));
+    const int e = mx_scale_byte(am);
+    const uint2 w = mx_pack8(v, e);
+    const uint32_t sd = mx_gather_scales(e, lane);
+    if (c < C) {
+      *reinterpret_cast<uint2*>(q + (long)c * ldq + r0 + ch * 8) = w;
+      if (ch == 0) s[(long)(r0 >> 7) * C + c] = sd;
+    }
+  }
+}
+
+// epilogue 16-B path legal for g (8-element groups of C / residual / aux / bias rows stay 16-B aligned)
+bool epi_vec(const dfk_gemm_args& g) {
+  return !g.c_f32 && aligned16(g.c) && g.ldc % 8 == 0 && g.cbs0 % 8 == 0 && g.cbs1 % 8 == 0 &&
+         (!g.bias || (aligned16(g.bias) && g.bias_bs1 % 8 == 0)) &&
+         (!g.residual || (aligned16(g.residual) && g.ldr % 8 == 0 && g.rbs0 % 8 == 0 && g.rbs1 % 8 == 0)) &&
+         (!g.aux || (aligned16(g.aux) && g.ldaux % 8 == 0));
+}
+
 }  // namespace
 
 extern "C" int dfk_gemm(const dfk_gemm_args* g, hipStream_t s) {
-  if (!g) return DFK_EINVAL;
+  if (!g || g->mx_q) return DFK_EINVAL;   // the MX copy of C is a dfk_gemm_mx epilogue
   return g->dtype == DFK_BF16 ? launch<bf16raw>(*g, s) : launch<float>(*g, s);
 }
 
@@ -909,6 +1165,69 @@ extern "C" int dfk_colsum(const void* x, int dtype, int64_t rows, int64_t cols, 
   else
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)x, (long)rows, (int)cols,
                        (long)ld, rows_per, out);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_gemm_mx(const dfk_gemm_args* gp, const dfk_mx_operand* a, const dfk_mx_operand* b, hipStream_t s) {
+  if (!gp || !a || !b) return DFK_EINVAL;
+  const dfk_gemm_args& g = *gp;
+  if (!a->q || !a->s || !b->q || !b->s || !g.c) return DFK_EINVAL;
+  if (g.dtype != DFK_BF16 || g.splitk != 1 || g.atomic || g.c_f32 || g.rowsum || g.nz0 != 1 || g.nz1 != 1)
+    return DFK_EINVAL;
+  if (g.K <= 0 || g.K % 128 || a->ld % 16 || b->ld % 16 || a->ld < g.K || b->ld < g.K) return DFK_EINVAL;
+  if (a->lds < g.M || b->lds < g.N) return DFK_EINVAL;
+  if (g.act < 0 || g.act > 2 || (g.act == 2 && !g.aux)) return DFK_EINVAL;
+  if (g.drop.mode && (!g.drop.rng || !(g.drop.p >= 0.f && g.drop.p < 1.f))) return DFK_EINVAL;
+  if (g.M <= 0 || g.N <= 0) return 0;
+  if ((long)(g.M - 1) * a->ld + g.K >= 0x7fffffffL || (long)(g.N - 1) * b->ld + g.K >= 0x7fffffffL) return DFK_EINVAL;
+  const bool mxo = g.mx_q != nullptr;
+  if (mxo && (!g.mx_s || g.N % 128 || g.mx_ldq % 16 || g.mx_ldq < g.N || g.mx_lds < g.M ||
+              (reinterpret_cast<uintptr_t>(g.mx_q) & 15)))
+    return DFK_EINVAL;
+  const long tiles128 = (long)dfk_cdiv(g.N, 128) * dfk_cdiv(g.M, 128);
+  const int evec = epi_vec(g) ? 1 : 0;
+  if (tiles128 < 1024) {   // 64 x 64 tiles for grids that 128 x 128 tiles cannot spread over the chip
+    dim3 grid(dfk_cdiv(g.N, 64), dfk_cdiv(g.M, 64));
+    if (grid.y > 65535) return DFK_EINVAL;
+    if (mxo) hipLaunchKernelGGL((gemm_mx_kernel<32, 2, 2, 2, true>), grid, dim3(256), 0, s, g, *a, *b, evec);
+    else hipLaunchKernelGGL((gemm_mx_kernel<32, 2, 2, 2, false>), grid, dim3(256), 0, s, g, *a, *b, evec);
+  } else {
+    dim3 grid(dfk_cdiv(g.N, 128), dfk_cdiv(g.M, 128));
+    if (grid.y > 65535) return DFK_EINVAL;
+    if (mxo) hipLaunchKernelGGL((gemm_mx_kernel<64, 2, 2, 2, true>), grid, dim3(256), 0, s, g, *a, *b, evec);
+    else hipLaunchKernelGGL((gemm_mx_kernel<64, 2, 2, 2, false>), grid, dim3(256), 0, s, g, *a, *b, evec);
+  }
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_mx_quant(const void* x, int dtype, int64_t rows, int64_t cols, int64_t ldx, int transpose,
+                            uint8_t* q, int64_t ldq, uint32_t* sc, hipStream_t s) {
+  if (!x || !q || !sc || rows < 0 || cols < 0 || (dtype != DFK_BF16 && dtype != DFK_F32)) return DFK_EINVAL;
+  if (ldq % 16 || (reinterpret_cast<uintptr_t>(q) & 15)) return DFK_EINVAL;
+  if (rows == 0 || cols == 0) return 0;
+  if (!transpose) {
+    if (cols % 128 || ldq < cols || ldx < cols || ldx % 8 || (reinterpret_cast<uintptr_t>(x) & 15)) return DFK_EINVAL;
+    const long threads = rows * (cols / 8);
+    const unsigned blocks = (unsigned)dfk_cdiv(threads, 256);
+    if (dtype == DFK_BF16)
+      hipLaunchKernelGGL(mx_quant_kernel<bf16raw>, dim3(blocks), dim3(256), 0, s, (const bf16raw*)x, (long)rows,
+                         (int)cols, (long)ldx, q, (long)ldq, sc);
+    else
+      hipLaunchKernelGGL(mx_quant_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, (long)rows, (int)cols,
+                         (long)ldx, q, (long)ldq, sc);
+  } else {
+    if (rows % 128 || ldq < rows || ldx < cols || rows > 0x7fffffff || cols > 0x7fffffff) return DFK_EINVAL;
+    dim3 grid(dfk_cdiv(cols, 64), (unsigned)(rows / 128));
+    if (grid.y > 65535) return DFK_EINVAL;
+    if (dtype == DFK_BF16)
+      hipLaunchKernelGGL(mx_quant_t_kernel<bf16raw>, grid, dim3(256), 0, s, (const bf16raw*)x, (int)rows, (int)cols,
+                         (long)ldx, q, (long)ldq, sc);
+    else
+      hipLaunchKernelGGL(mx_quant_t_kernel<float>, grid, dim3(256), 0, s, (const float*)x, (int)rows, (int)cols,
+                         (long)ldx, q, (long)ldq, sc);
+  }
   DFK_CHECK_LAUNCH();
   return 0;
 }

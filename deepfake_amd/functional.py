@@ -102,21 +102,37 @@ def rows2d(x):
     return x.reshape(-1, x.shape[-1])
 
 
+def mx_weight(p, transpose=False):
+    """MX-fp8 operand of a Linear weight [N, K] from its fp32 master: along K (the forward's B operand) or, with
+    transpose, W^T along N (the dX GEMM's B operand).  Quantised per call, so a replayed graph always reads the
+    weights SGD just wrote."""
+    return K.mx_quant(_orig(p).detach(), transpose=transpose)
+
+
+def mx_ok(x, weight, mx):
+    """The MX-fp8 path applies: requested, bf16 activations, K and N multiples of 128."""
+    return bool(mx) and x.dtype == torch.bfloat16 and x.shape[-1] % 128 == 0 and weight.shape[0] % 128 == 0
+
+
 class LinearFn(torch.autograd.Function):
     """y = drop(x W^T + b) (act 1: drop(gelu(.))) (+ residual).  nn.Linear / F.linear, with the
-    dropout / DropPath that follows it in the reference (rng.Drop spec, applied before the residual add)."""
+    dropout / DropPath that follows it in the reference (rng.Drop spec, applied before the residual add).
+    mx: the forward and the input-gradient GEMMs run on MX-fp8 operands (dfk_gemm_mx; C4's fp8 path), the
+    weight gradient stays bf16."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, act, residual, drop=None):
+    def forward(ctx, x, weight, bias, act, residual, drop=None, mx=False):
         dt = x.dtype
-        w = compute_weight(weight, dt)
         b = compute_weight(bias, dt)
         aux = torch.empty(x.shape[0], weight.shape[0], device=x.device, dtype=dt) if act == 1 else None
-        y = K.linear(x, w, b, act=act, aux=aux, residual=residual, drop=drop)
+        if mx:
+            y = K.gemm_mx(K.mx_quant(x), mx_weight(weight), bias=b, act=act, aux=aux, residual=residual, drop=drop)
+        else:
+            y = K.linear(x, compute_weight(weight, dt), b, act=act, aux=aux, residual=residual, drop=drop)
         grad_use(ctx, 1, weight)
         grad_use(ctx, 2, bias)
         ctx.save_for_backward(x, weight, bias, aux)
-        ctx.act, ctx.has_bias, ctx.has_res, ctx.drop = act, bias is not None, residual is not None, drop
+        ctx.act, ctx.has_bias, ctx.has_res, ctx.drop, ctx.mx = act, bias is not None, residual is not None, drop, mx
         return y
 
     @staticmethod
@@ -125,8 +141,12 @@ class LinearFn(torch.autograd.Function):
         dy = dy.contiguous()
         dz = K.dropout(dy, ctx.drop) if ctx.drop is not None else dy
         dz = K.gelu_bwd(dz, aux) if ctx.act == 1 else dz
-        w = compute_weight(weight, x.dtype)
-        dx = K.linear_dx(dz, w) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if ctx.mx:
+                dx = K.gemm_mx(K.mx_quant(dz), mx_weight(weight, transpose=True))
+            else:
+                dx = K.linear_dx(dz, compute_weight(weight, x.dtype))
         dw = db = None
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
@@ -136,13 +156,14 @@ class LinearFn(torch.autograd.Function):
             db = K.colsum(dz, grad_sink(bias))
         if want_b:
             db = grad_done(bias, db)
-        return dx, dw, db, None, (dy if ctx.has_res else None), None
+        return dx, dw, db, None, (dy if ctx.has_res else None), None, None
 
 
-def linear(x, weight, bias=None, act=0, residual=None, drop=None):
+def linear(x, weight, bias=None, act=0, residual=None, drop=None, mx=False):
     shp = x.shape
-    y = LinearFn.apply(rows2d(x).contiguous(), weight, bias, act,
-                       rows2d(residual).contiguous() if residual is not None else None, drop)
+    x2 = rows2d(x).contiguous()
+    y = LinearFn.apply(x2, weight, bias, act, rows2d(residual).contiguous() if residual is not None else None, drop,
+                       mx_ok(x2, weight, mx))
     return y.view(*shp[:-1], weight.shape[0])
 
 
@@ -233,17 +254,22 @@ class MlpFn(torch.autograd.Function):
     block's other consumer of x (SwinV2's post-norm residual): its gradient is added in the same epilogue."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, residual, drop_act=None, drop_out=None, res_is_input=False, skip=False):
+    def forward(ctx, x, w1, b1, w2, b2, residual, drop_act=None, drop_out=None, res_is_input=False, skip=False,
+                mx=False):
         dt = x.dtype
-        W1, B1, W2, B2 = (compute_weight(t, dt) for t in (w1, b1, w2, b2))
+        B1, B2 = compute_weight(b1, dt), compute_weight(b2, dt)
         pre = torch.empty(x.shape[0], w1.shape[0], device=x.device, dtype=dt)
-        h = K.linear(x, W1, B1, act=1, aux=pre, drop=drop_act)
-        y = K.linear(h, W2, B2, residual=residual, drop=drop_out)
+        if mx:   # MX-fp8 GEMMs; the fc1 epilogue also writes h quantised for fc2 (no separate pass)
+            h, hq = K.gemm_mx(K.mx_quant(x), mx_weight(w1), bias=B1, act=1, aux=pre, drop=drop_act, mx_out=True)
+            y = K.gemm_mx(hq, mx_weight(w2), bias=B2, residual=residual, drop=drop_out)
+        else:
+            h = K.linear(x, compute_weight(w1, dt), B1, act=1, aux=pre, drop=drop_act)
+            y = K.linear(h, compute_weight(w2, dt), B2, residual=residual, drop=drop_out)
         for i, p in enumerate((w1, b1, w2, b2)):
             grad_use(ctx, 1 + i, p)
         ctx.save_for_backward(x, w1, b1, w2, b2, pre, h)
         ctx.has_res, ctx.drop_act, ctx.drop_out = residual is not None, drop_act, drop_out
-        ctx.res_is_input, ctx.skip = res_is_input, skip
+        ctx.res_is_input, ctx.skip, ctx.mx = res_is_input, skip, mx
         if skip:
             return y, x.view_as(x)
         return y
@@ -256,27 +282,35 @@ class MlpFn(torch.autograd.Function):
         if ctx.drop_out is not None:
             dy = K.dropout(dy, ctx.drop_out)
         dt = x.dtype
-        dpre = K.linear_dx(dy, compute_weight(w2, dt), act=2, aux=pre, drop=ctx.drop_act)   # (dy W2).Z * gelu'(pre)
+        extra = dyr if ctx.res_is_input else (dskip if ctx.skip else None)
+        if ctx.mx:   # (dy W2).Z * gelu'(pre) with its MX copy from the same epilogue, then dpre W1 on MX operands
+            dpre, dpreq = K.gemm_mx(K.mx_quant(dy), mx_weight(w2, transpose=True), act=2, aux=pre, drop=ctx.drop_act,
+                                    mx_out=True)
+            dx = K.gemm_mx(dpreq, mx_weight(w1, transpose=True),
+                           residual=extra.contiguous() if extra is not None else None) \
+                if ctx.needs_input_grad[0] else None
+        else:
+            dpre = K.linear_dx(dy, compute_weight(w2, dt), act=2, aux=pre, drop=ctx.drop_act)   # (dy W2).Z * gelu'(pre)
+            dx = K.linear_dx(dpre, compute_weight(w1, dt), residual=extra) if ctx.needs_input_grad[0] else None
         db2 = grad_sink(b2)
         dw2 = grad_done(w2, K.linear_dw(dy, h, grad_sink(w2), db=db2))
         db2 = grad_done(b2, db2)
-        extra = dyr if ctx.res_is_input else (dskip if ctx.skip else None)
-        dx = K.linear_dx(dpre, compute_weight(w1, dt), residual=extra) if ctx.needs_input_grad[0] else None
         db1 = grad_sink(b1)
         dw1 = grad_done(w1, K.linear_dw(dpre, x, grad_sink(w1), db=db1))
         db1 = grad_done(b1, db1)
         dres = dyr if (ctx.has_res and not ctx.res_is_input) else None
-        return dx, dw1, db1, dw2, db2, dres, None, None, None, None
+        return dx, dw1, db1, dw2, db2, dres, None, None, None, None, None
 
 
-def mlp(x, fc1, fc2, residual=None, drop_act=None, drop_out=None, skip=False):
+def mlp(x, fc1, fc2, residual=None, drop_act=None, drop_out=None, skip=False, mx=False):
     """Mlp(x) (+ residual).  skip=True also returns an alias of x for the block's other consumer of x, whose
-    gradient then joins dx inside the fc1 dX GEMM."""
+    gradient then joins dx inside the fc1 dX GEMM.  mx: MX-fp8 forward / dX GEMMs (C4's fp8 path)."""
     shp = x.shape
     x2 = rows2d(x).contiguous()
     res_is_input = residual is not None and residual is x
     r2 = x2 if res_is_input else (rows2d(residual).contiguous() if residual is not None else None)
-    out = MlpFn.apply(x2, fc1.weight, fc1.bias, fc2.weight, fc2.bias, r2, drop_act, drop_out, res_is_input, skip)
+    mx = mx_ok(x2, fc1.weight, mx) and fc2.weight.shape[0] % 128 == 0
+    out = MlpFn.apply(x2, fc1.weight, fc1.bias, fc2.weight, fc2.bias, r2, drop_act, drop_out, res_is_input, skip, mx)
     if skip:
         y, xs = out
         return y.view(*shp[:-1], fc2.weight.shape[0]), xs.view(shp)

@@ -80,6 +80,85 @@ def linear(x, w, b=None, act=0, aux=None, residual=None, out=None, beta=0.0, dro
     return out
 
 
+class MxTensor:
+    """An MX-fp8 operand (include/dfk.h dfk_mx_operand): e4m3 values q [rows, K] (uint8, K contiguous) and the
+    E8M0 block scales s [K/128, rows] (int32: four bytes = the four 32-blocks of one 128-k tile)."""
+
+    def __init__(self, q, s):
+        self.q, self.s = q, s
+
+    @property
+    def shape(self):
+        return tuple(self.q.shape)
+
+    def operand(self):
+        o = L.MxOperand()
+        o.q, o.s = self.q.data_ptr(), self.s.data_ptr()
+        o.ld, o.lds = int(self.q.stride(0)), int(self.s.stride(0))
+        return o
+
+
+def mx_quant(x, transpose=False):
+    """x [rows, cols] (bf16 / fp32, unit stride along cols) -> MxTensor along cols ([rows, cols]), or along rows
+    of x^T (transpose=True: [cols, rows]; the dX GEMM's W^T)."""
+    rows, cols = x.shape
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    R, Kd = (cols, rows) if transpose else (rows, cols)
+    if Kd % 128:
+        raise ValueError(f"mx_quant: the quantised dim ({Kd}) must be a multiple of 128")
+    q = torch.empty(R, Kd, device=x.device, dtype=torch.uint8)
+    s = torch.empty(Kd // 128, R, device=x.device, dtype=torch.int32)
+    L.check(L.lib().dfk_mx_quant(L.ptr(x), L.dt(x), rows, cols, x.stride(0), int(transpose), L.ptr(q), q.stride(0),
+                                 L.ptr(s), L.stream()), "mx_quant")
+    return MxTensor(q, s)
+
+
+def mx_empty(rows, K, device):
+    return MxTensor(torch.empty(rows, K, device=device, dtype=torch.uint8),
+                    torch.empty(K // 128, rows, device=device, dtype=torch.int32))
+
+
+def gemm_mx(a, b, out=None, bias=None, act=0, aux=None, residual=None, drop=None, beta=0.0, mx_out=False):
+    """out [M, N] bf16 = A B^T (+ the dfk_gemm epilogue) with A [M, K], B [N, K] MxTensors (dfk_gemm_mx).
+    mx_out=True: also return the output quantised along N (the next MX GEMM's A operand), from the same
+    epilogue: (out, MxTensor)."""
+    M, Kd = a.shape
+    N = b.shape[0]
+    if b.shape[1] != Kd:
+        raise ValueError(f"gemm_mx: K mismatch {a.shape} x {b.shape}")
+    if out is None:
+        out = torch.empty(M, N, device=a.q.device, dtype=torch.bfloat16)
+    g = L.GemmArgs()
+    if drop is not None:
+        g.drop = L.drop(drop, out.device)
+    g.c = out.data_ptr()
+    g.bias = bias.data_ptr() if bias is not None else None
+    g.residual = residual.data_ptr() if residual is not None else None
+    g.aux = aux.data_ptr() if aux is not None else None
+    g.ldc = int(out.stride(0))
+    g.ldr = int(residual.stride(0)) if residual is not None else 0
+    g.ldaux = int(aux.stride(0)) if aux is not None else 0
+    g.M, g.N, g.K = int(M), int(N), int(Kd)
+    g.dtype = L.BF16
+    g.nz0 = g.nz1 = 1
+    g.splitk = 1
+    g.act = int(act)
+    g.beta = float(beta)
+    for t in (bias, residual, aux):
+        if t is not None and t.dtype != torch.bfloat16:
+            raise TypeError("gemm_mx: the epilogue operands are bf16")
+    mo = None
+    if mx_out:
+        if N % 128:
+            raise ValueError(f"gemm_mx: an MX copy of the output needs N % 128 == 0 (N={N})")
+        mo = mx_empty(M, N, out.device)
+        g.mx_q, g.mx_s = mo.q.data_ptr(), mo.s.data_ptr()
+        g.mx_ldq, g.mx_lds = int(mo.q.stride(0)), int(mo.s.stride(0))
+    L.check(L.lib().dfk_gemm_mx(g, a.operand(), b.operand(), L.stream()), f"gemm_mx M={M} N={N} K={Kd}")
+    return (out, mo) if mx_out else out
+
+
 def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None, residual=None):
     """dx[M,K] = dy[M,N] @ w[N,K]  (act=2: times gelu'(aux)) (drop: times the forward's dropout mask)
     (+ residual[M,K]: the gradient the input receives along a skip path, added in the epilogue)."""

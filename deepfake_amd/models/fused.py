@@ -5,14 +5,14 @@ SwinTransformer3D (+ mean pooling, VSTFeat), mel slot SwinTransformerV2
 CONFIGS mirror BASELINE.json: C1 = tiny VST 2,2,2,2 / window 4x7x7 + reduced
 mel SwinV2 + 2-layer wav2vec2 (8x112x112, 1 s); C2 = Swin-T 2,2,6,2 / window
 8x7x7 + SwinV2 (128; 2,2,18,2) + wav2vec2-base (32x224x224, 4 s); C4 =
-Swin-B video; C5 = 64 frames + 10 s audio.
+Swin-B video (fp8=True: MX-fp8 GEMMs in its stages 3-4); C5 = 64 frames + 10 s audio.
 """
 import os
 import types
 
 import torch
 
-from . import set_compute_dtype
+from . import set_compute_dtype, set_fp8
 from .audioTransformer import Audio2D
 from .ModalFusion import FusionModel
 from .swin_transformer2d import SwinTransformerV2
@@ -45,7 +45,7 @@ CONFIGS = {
 }
 
 
-def build_fused(cfg, args=None, w2v_config=W2V_CONFIG, compute_dtype=torch.float32, regularize=False):
+def build_fused(cfg, args=None, w2v_config=W2V_CONFIG, compute_dtype=torch.float32, regularize=False, fp8=False):
     """The north-star fused model.  regularize=False (parity / default): every dropout, DropPath,
     SpecAugment and LayerDrop off (Q12).  regularize=True: the reference's training regularisers — VST
     drop_path_rate 0.2 (SwinTransformer3D default, video_swin_transformer.py:500), SwinV2 0.1
@@ -66,6 +66,8 @@ def build_fused(cfg, args=None, w2v_config=W2V_CONFIG, compute_dtype=torch.float
     pa = Audio2D(args, Wav2Vec2Model(wcfg), num_classes=1, use_feat=True)
     m = FusionModel(args, VSTFeat(vst), mel, pa, out_dim=1, video_dim=cfg["video_dim"], audio_dim=cfg["audio_dim"],
                     paudio_dim=768)
+    if fp8:   # C4: MX-fp8 video-trunk GEMMs (bf16 compute everywhere else)
+        set_fp8(m, cfg.get("fp8_stages", (2, 3)))
     return set_compute_dtype(m, compute_dtype)
 
 

@@ -135,13 +135,14 @@ class SwinTransformerBlock3D(nn.Module):
         self.dp = (rng.Drop(drop_path, mode=2), rng.Drop(drop_path, mode=2)) if drop_path > 0 else None
         self.norm2 = norm_layer(dim)
         self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
+        self.mx = False   # MX-fp8 qkv / proj / fc1 / fc2 GEMMs (models.set_fp8; C4's fp8 path)
 
     def _part1(self, xn, dims):
         """qkv -> shifted-window attention (pad/roll/partition in-kernel) of LN1's output; pre-proj rows."""
         B, D, H, W = dims
         C = xn.shape[-1]
         ws, ss = get_window_size((D, H, W), self.window_size, self.shift_size)
-        qkv = Fn.linear(xn.reshape(-1, C), self.attn.qkv.weight, self.attn.qkv.bias)
+        qkv = Fn.linear(xn.reshape(-1, C), self.attn.qkv.weight, self.attn.qkv.bias, mx=self.mx)
         return self.attn.core(qkv, (B, D, H, W), ws, ss)
 
     def forward_part1(self, x, mask_matrix=None):
@@ -155,12 +156,12 @@ class SwinTransformerBlock3D(nn.Module):
         xn, xs = Fn.layer_norm(x, self.norm1, skip=True)
         o = self._part1(xn, (B, D, H, W))
         return Fn.linear(o, self.attn.proj.weight, self.attn.proj.bias, residual=xs.reshape(-1, C),
-                         drop=dp).view(B, D, H, W, C)
+                         drop=dp, mx=self.mx).view(B, D, H, W, C)
 
     def _mlp_branch(self, x, dp):
         """x + DropPath(mlp(LN2 x))  (forward_part2 + the second residual, :273-276)."""
         xn, xs = Fn.layer_norm(x, self.norm2, skip=True)
-        return Fn.mlp(xn, self.mlp.fc1, self.mlp.fc2, residual=xs, drop_out=dp)
+        return Fn.mlp(xn, self.mlp.fc1, self.mlp.fc2, residual=xs, drop_out=dp, mx=self.mx)
 
     def forward(self, x, mask_matrix=None):
         B, D, H, W, C = x.shape

@@ -99,12 +99,41 @@ typedef struct {
                            of a Linear when A = dy^T, computed by one extra MFMA against a ones operand */
   dfk_drop drop;        /* dropout / DropPath of the output before the residual add (bf16/f32 C only) */
   float alpha;          /* scale of the product (+bias) before the residual add; 0 = 1 */
+  uint8_t* mx_q;        /* dfk_gemm_mx only (NULL elsewhere): also write the bf16 C, quantised along N, as an MX
+                           operand (see dfk_mx_operand below; N % 128 == 0) — the next MX GEMM's input */
+  uint32_t* mx_s;
+  int64_t mx_ldq, mx_lds;
 } dfk_gemm_args;
 int dfk_gemm(const dfk_gemm_args* g, hipStream_t stream);
 /* Bytes of scratch dfk_gemm wants in g->ws: grids too small to fill the chip (the
  * wav2vec2 / SwinV2-stage-3 Linears, M ~ 1.6k rows) are split along K into fp32
  * slabs that a second kernel sums before the epilogue.  0 = no split. */
 int64_t dfk_gemm_workspace(const dfk_gemm_args* g);
+
+/* ---- MX-fp8 (OCP microscaling) GEMM path of the C4 Swin-B video trunk (BASELINE configs[3]: "fp8 MFMA
+ * attention/QKV path"): the qkv / proj / fc1 / fc2 Linears of video_swin_transformer.py:134-136 (WindowAttention3D)
+ * and src/utils.py:249-251 (Mlp) — forward y = x W^T and input gradient dx = dy W — on the block-scaled
+ * v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate).  The weight gradient stays bf16.
+ * An MX operand holds a [rows][K] matrix, K contiguous: OCP e4m3 (e4m3fn) values q (row stride ld bytes) and one
+ * E8M0 scale per 32 consecutive k; the four scales of k-tile t (k in [128t, 128t+128)) of row r are the bytes of
+ * the dword s[t*lds + r] (byte j: k-block 4t + j).  Element value = e4m3(q) * 2^(scale - 127).  K % 128 == 0. */
+typedef struct {
+  const uint8_t* q;
+  const uint32_t* s;
+  int64_t ld;           /* bytes between rows of q (multiple of 16) */
+  int64_t lds;          /* dwords between k-tiles of s (>= rows) */
+} dfk_mx_operand;
+/* Quantise x [rows][cols] (dtype bf16 or f32, row stride ldx elements) to an MX operand along cols (transpose = 0:
+ * q [rows][cols], s [cols/128][lds = rows]; cols % 128 == 0), or x^T along rows (transpose = 1: q [cols][rows],
+ * s [rows/128][lds = cols]; rows % 128 == 0) — the dx GEMM's weight operand W^T.  Per 32-element block: scale
+ * exponent e = the smallest with amax / 2^e <= 448 (e4m3's largest finite value, so nothing saturates), values
+ * x / 2^e rounded to nearest even (v_cvt_pk_fp8_f32); an all-zero block gets scale 2^0. */
+int dfk_mx_quant(const void* x, int dtype, int64_t rows, int64_t cols, int64_t ldx, int transpose, uint8_t* q,
+                 int64_t ldq, uint32_t* s, hipStream_t stream);
+/* C [M][N] = A B^T (+ g's epilogue: bias / GELU with aux / dGELU / dropout / residual, bf16 output) with A [M][K]
+ * and B [N][K] MX operands.  g supplies M, N, K and the epilogue fields only: dtype DFK_BF16, no split-K, no atomic,
+ * no fp32 C, no rowsum, no batching; g->a / g->b are ignored.  K % 128 == 0. */
+int dfk_gemm_mx(const dfk_gemm_args* g, const dfk_mx_operand* a, const dfk_mx_operand* b, hipStream_t stream);
 
 /* out[j] (+)= sum_i x[i*ld + j] (fp32 atomics).  Linear bias gradients. */
 int dfk_colsum(const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld, float* out, hipStream_t stream);

@@ -70,6 +70,12 @@ BLOCK_C2_S1 = dict(name="block_c2_s1", dim=96, heads=3, window=(8, 7, 7), shift=
 # stage 4: H=W=7 <= window -> get_window_size keeps only the D shift (4,0,0) (Q6); 2 windows along D
 BLOCK_C2_S4 = dict(name="block_c2_s4", dim=768, heads=24, window=(8, 7, 7), shift=(4, 3, 3), shape=(1, 16, 7, 7),
                    seed=161)
+# C4 (Swin-B video trunk, BASELINE configs[3]): stage 1 (dim 128, 4 heads, N=392, shift 4x3x3, a whole clip's
+# 16x56x56 volume) and stage 3 (dim 512, 16 heads, 16x14x14: 8 windows, shift 4x3x3) — the bf16 and MX-fp8 blocks
+BLOCK_C4_S1 = dict(name="block_c4_s1", dim=128, heads=4, window=(8, 7, 7), shift=(4, 3, 3), shape=(1, 16, 56, 56),
+                   seed=191)
+BLOCK_C4_S3 = dict(name="block_c4_s3", dim=512, heads=16, window=(8, 7, 7), shift=(4, 3, 3), shape=(1, 16, 14, 14),
+                   seed=195)
 # SwinV2-B mel stage 3 (C2 mel branch): 14x14 tokens, C=512, 16 heads, window 7, blocks shift 0 / 3,
 # pretrained_window_size 16 (the CPB-MLP coordinate normalisation), two clips
 MEL_C2_S3 = dict(name="mel_c2_s3", dim=512, heads=16, res=(14, 14), window=7, pretrained=16, B=2, seed=171)

@@ -93,6 +93,13 @@ def case_block_c2():
     _block(GC.BLOCK_C2_S4)
 
 
+def case_block_c4():
+    """C4 geometry (Swin-B video trunk): stage 1 (dim 128, 4 heads, N=392, shift 4x3x3) and stage 3 (dim 512,
+    16 heads) — the blocks whose Linears the fp8 path runs on MX-fp8 GEMMs."""
+    _block(GC.BLOCK_C4_S1)
+    _block(GC.BLOCK_C4_S3)
+
+
 def case_mel_c2():
     """SwinV2-B mel stage-3 block pair (reference BasicLayer: W-MSA then SW-MSA shift 3)."""
     c = GC.MEL_C2_S3
@@ -376,6 +383,6 @@ if __name__ == "__main__":
     only = sys.argv[1:]
     for fn in [case_window_attention, case_block, case_patch_embed_merge, case_vst_c1, case_w2v, case_head,
                case_fused_c1, case_block_c2, case_mel_c2, case_fused_c1_grads, case_fused_c2, case_state_keys,
-               case_config_flags, case_inception]:
+               case_config_flags, case_inception, case_block_c4]:
         if not only or fn.__name__ in only:
             fn()

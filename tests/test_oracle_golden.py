@@ -39,7 +39,7 @@ def test_window_attention(c):
     _grads(fx, m)
 
 
-@pytest.mark.parametrize("c", GC.BLOCK_CASES, ids=lambda c: c["name"])
+@pytest.mark.parametrize("c", GC.BLOCK_CASES + [GC.BLOCK_C4_S3], ids=lambda c: c["name"])
 def test_block(c):
     fx = load(c["name"])
     m = named_fill_(V.SwinTransformerBlock3D(c["dim"], c["heads"], c["window"], c["shift"]), c["seed"])
