@@ -89,7 +89,7 @@ def time_kernel(fn, iters):
     return s.elapsed_time(e) / iters * 1e-3   # seconds per launch
 
 
-ROOFLINE_KERNEL = "wattn_fwd3_kernel<32, true, false>"
+ROOFLINE_KERNEL = "wattn_fwd4_kernel<32, false, 2>"
 ROOFLINE_PMC = os.path.join(HERE, "profiles", "r3o_wattn_fwd_pmc.json")
 
 
@@ -122,7 +122,7 @@ def roofline_case(cfg, B, dt):
     out = torch.empty(rows, C, device="cuda", dtype=dt)
     args = (qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, (B, D, H, W), win, win, shift, heads, hd, hd ** -0.5)
     # the bf16 score-bias tiles (dfk_wattn_table, a separate launch) are built once: the timed launch is the
-    # attention kernel alone, the one rocprofv3 lists as wattn_fwd3_kernel<32, true, false>
+    # attention kernel alone, the one rocprofv3 lists as wattn_fwd4_kernel<32, false, 2>
     _, _, tab = K.wattn_fwd(*args, rpb=rpb, out=out, return_table=True)
 
     def run():

@@ -70,6 +70,12 @@ class PatchEmbedArgs(C.Structure):
                 ("dw", C.c_void_p), ("db", C.c_void_p), ("dln_w", C.c_void_p), ("dln_b", C.c_void_p)]
 
 
+class PilResize(C.Structure):
+    _fields_ = [("H", C.c_int32), ("W", C.c_int32), ("cin", C.c_int32), ("out_h", C.c_int32), ("out_w", C.c_int32),
+                ("xb", C.c_void_p), ("xk", C.c_void_p), ("kx", C.c_int32),
+                ("yb", C.c_void_p), ("yk", C.c_void_p), ("ky", C.c_int32)]
+
+
 class Conv2dGeo(C.Structure):
     _fields_ = [("N", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("C", C.c_int32), ("kh", C.c_int32),
                 ("kw", C.c_int32), ("sh", C.c_int32), ("sw", C.c_int32), ("ph", C.c_int32), ("pw", C.c_int32),
@@ -127,8 +133,8 @@ SIGNATURES = {
     "dfk_mel_workspace": [_I64, _I64, _I32, _I32, _I32],
     "dfk_mel_image": [_VP, _I64, _I64, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP],
     "dfk_gray_normalize": [_VP, _VP, _I64, _I32, _I32, C.POINTER(C.c_float), C.POINTER(C.c_float), _VP],
-    "dfk_frame_augment": [_VP, _I64, _I32, _I32, _I32, _I32, _VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float),
-                          _VP, _VP],
+    "dfk_frame_augment": [_VP, _I64, C.POINTER(PilResize), _VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                          _VP, _VP, _VP],
     "dfk_layerdrop_flags": [C.POINTER(Drop), _I32, _VP, _VP, _VP],
     "dfk_spec_augment_fwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _F, _I32, _I32, C.POINTER(Drop), C.c_int, _VP],
     "dfk_spec_augment_bwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, C.c_int, _VP],

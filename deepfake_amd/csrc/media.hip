@@ -14,12 +14,10 @@
 //    waveform at the rate the filterbank was built for).
 //  * gray image -> model input — Image.convert('RGB') + T.ToTensor() + T.Normalize (data_process.py:55-69,162):
 //    uint8 [N, H, W] -> fp32 [N, 3, H, W], (x / 255 - mean[c]) / std[c].
-//  * train-time frame augmentation — T.Resize((224,224)), T.RandomHorizontalFlip, T.RandomVerticalFlip,
-//    T.RandomRotation(90), T.ToTensor, T.Normalize (data_process.py:62-69) on decoded RGB frames, fused into
-//    one gather per output pixel: rotation (torchvision F.rotate on tensors: inverse affine grid of pixel
-//    centres, grid_sample nearest, fill 0) of the flipped, resized frame (bilinear, half-pixel centres, rounded
-//    to uint8), then normalised.  Random flips and angles are per frame (the reference transforms each frame
-//    separately) and come in as device arrays.
+//  * frame / mel-image transform — torchvision's T.Resize / RandomHorizontalFlip / RandomVerticalFlip /
+//    RandomRotation(90) / ToTensor / Normalize as the reference runs them, on PIL images (data_process.py:55-69,
+//    162; src/utils.py:32-33): PIL's antialiased BILINEAR resize (width pass, then height pass fused with the flips,
+//    the NEAREST rotation's fixed-point inverse map and the normalisation).  Random flips / angles are per image.
 #include "common.h"
 
 namespace {
@@ -141,60 +139,91 @@ __global__ __launch_bounds__(256) void gray_norm_kernel(const uint8_t* __restric
   out[2 * (long)HW] = (x - m2) / s2;
 }
 
-struct AugArgs {
-  int H, W, oh, ow;
+// ---- train-time frame transform, PIL semantics (data_process.py:62-69 on PIL images, src/utils.py:32-33) ----
+// T.Resize((h, w)) on a PIL image is Image.resize(BILINEAR): PIL's two-pass separable resampling — a triangle
+// filter whose support grows with the downscale factor (antialiased), coefficients normalised per output
+// pixel and rounded to 22-bit fixed point (precompute_coeffs + normalize_coeffs_8bpc; built on the host,
+// media.pil_bilinear_coeffs), the width pass first into uint8, then the height pass, each output rounded
+// (+2^21) and clipped to uint8.  Flips are exact; T.RandomRotation on a PIL image is Image.rotate(NEAREST,
+// fill 0): the 16.16 fixed-point inverse affine walk of PIL's affine_fixed (matrix built on the host exactly as
+// PIL builds it, media.pil_rotate_fixed).  Then ToTensor + Normalize.
+struct PilArgs {
+  int H, W, cin, oh, ow, kx, ky;
   float m[3], sd[3];
 };
 
-// resized pixel (y, x) channel c of the source frame: bilinear with half-pixel centres (torch
-// F.interpolate(bilinear, align_corners=False) source indices), rounded to uint8 as the PIL image is
-__device__ __forceinline__ float resized(const uint8_t* fr, const AugArgs& a, int y, int x, int c) {
-  if (a.H == a.oh && a.W == a.ow) return (float)fr[((long)y * a.W + x) * 3 + c];
-  const float sy = (float)a.H / a.oh, sx = (float)a.W / a.ow;
-  const float fy = fmaxf(sy * (y + 0.5f) - 0.5f, 0.f), fx = fmaxf(sx * (x + 0.5f) - 0.5f, 0.f);
-  const int y0 = (int)fy, x0 = (int)fx;
-  const int y1 = y0 + (y0 < a.H - 1), x1 = x0 + (x0 < a.W - 1);
-  const float ly = fy - y0, lx = fx - x0;
-  const float v00 = fr[((long)y0 * a.W + x0) * 3 + c], v01 = fr[((long)y0 * a.W + x1) * 3 + c];
-  const float v10 = fr[((long)y1 * a.W + x0) * 3 + c], v11 = fr[((long)y1 * a.W + x1) * 3 + c];
-  const float v = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
-  return fminf(fmaxf(rintf(v), 0.f), 255.f);
+// width pass: src [f][H][W][cin] -> tmp [f][H][ow][cin] (uint8); one thread per output pixel of a row
+__global__ __launch_bounds__(256) void pil_resize_w_kernel(const uint8_t* __restrict__ src, long frames, PilArgs a,
+                                                           const int* __restrict__ xb, const int* __restrict__ xk,
+                                                           uint8_t* __restrict__ tmp) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = frames * a.H * a.ow;
+  if (i >= n) return;
+  const int x = (int)(i % a.ow);
+  const long fr = i / a.ow;   // (frame, row)
+  const int x0 = xb[2 * x], cnt = xb[2 * x + 1];
+  const int* k = xk + (long)x * a.kx;
+  const uint8_t* row = src + fr * a.W * a.cin;
+  int s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
+  for (int t = 0; t < cnt; ++t) {
+    const uint8_t* px = row + (long)(x0 + t) * a.cin;
+    s0 += (int)px[0] * k[t];
+    if (a.cin == 3) {
+      s1 += (int)px[1] * k[t];
+      s2 += (int)px[2] * k[t];
+    }
+  }
+  uint8_t* o = tmp + i * a.cin;
+  o[0] = (uint8_t)min(max(s0 >> 22, 0), 255);
+  if (a.cin == 3) {
+    o[1] = (uint8_t)min(max(s1 >> 22, 0), 255);
+    o[2] = (uint8_t)min(max(s2 >> 22, 0), 255);
+  }
 }
 
-__global__ __launch_bounds__(256) void frame_augment_kernel(const uint8_t* __restrict__ src, long frames, AugArgs a,
-                                                            const int* __restrict__ flips,
-                                                            const float* __restrict__ angles, float* __restrict__ dst) {
+// height pass of the resized pixel (y, x) fused with flips, rotation, ToTensor and Normalize
+__global__ __launch_bounds__(256) void pil_augment_kernel(const uint8_t* __restrict__ tmp, long frames, PilArgs a,
+                                                          const int* __restrict__ yb, const int* __restrict__ yk,
+                                                          const int* __restrict__ flips, const int* __restrict__ aff,
+                                                          float* __restrict__ dst) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long per = (long)a.oh * a.ow;
   if (i >= frames * per) return;
   const long f = i / per;
   const int p = (int)(i % per), y = p / a.ow, x = p % a.ow;
-  const int fl = flips ? flips[f] : 0;
   int iy = y, ix = x;
   bool in = true;
-  if (angles && angles[f] != 0.f) {
-    // torchvision F.rotate (tensor): theta = [[cos, sin, 0], [-sin, cos, 0]] of rot = radians(-angle) applied
-    // to the centred pixel-centre grid, normalised by (w/2, h/2), unnormalised as grid_sample
-    // (align_corners=False), nearest = round half to even
-    const double rot = -(double)angles[f] * 3.14159265358979323846 / 180.0;
-    const float c = (float)cos(rot), s = (float)sin(rot);
-    const float bx = -a.ow * 0.5f + 0.5f + (float)x, by = -a.oh * 0.5f + 0.5f + (float)y;
-    const float gx = __fadd_rn(__fmul_rn(bx, c / (0.5f * a.ow)), __fmul_rn(by, s / (0.5f * a.ow)));
-    const float gy = __fadd_rn(__fmul_rn(bx, -s / (0.5f * a.oh)), __fmul_rn(by, c / (0.5f * a.oh)));
-    const float ux = ((gx + 1.f) * a.ow - 1.f) / 2.f, uy = ((gy + 1.f) * a.oh - 1.f) / 2.f;
-    ix = (int)rintf(ux);
-    iy = (int)rintf(uy);
+  if (aff && aff[8 * f]) {   // PIL affine_fixed: xx = a2 + x a0 + y a1, yy = a5 + x a3 + y a4 (16.16), >> 16
+    const int* m = aff + 8 * f;
+    const int xx = m[3] + x * m[1] + y * m[2], yy = m[6] + x * m[4] + y * m[5];
+    ix = xx >> 16;
+    iy = yy >> 16;
     in = ix >= 0 && ix < a.ow && iy >= 0 && iy < a.oh;
   }
+  const int fl = flips ? flips[f] : 0;
   if (fl & 2) iy = a.oh - 1 - iy;   // vertical flip (applied before the rotation)
   if (fl & 1) ix = a.ow - 1 - ix;   // horizontal flip (first)
-  const uint8_t* fr = src + f * (long)a.H * a.W * 3;
   float* out = dst + f * 3 * per + p;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const float v = in ? resized(fr, a, iy, ix, c) : 0.f;
-    out[(long)c * per] = (v / 255.f - a.m[c]) / a.sd[c];
+  int v[3] = {0, 0, 0};
+  if (in) {
+    const int y0 = yb[2 * iy], cnt = yb[2 * iy + 1];
+    const int* k = yk + (long)iy * a.ky;
+    const uint8_t* col = tmp + (f * a.H * a.ow + ix) * a.cin;
+    int s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
+    for (int t = 0; t < cnt; ++t) {
+      const uint8_t* px = col + (long)(y0 + t) * a.ow * a.cin;
+      s0 += (int)px[0] * k[t];
+      if (a.cin == 3) {
+        s1 += (int)px[1] * k[t];
+        s2 += (int)px[2] * k[t];
+      }
+    }
+    v[0] = min(max(s0 >> 22, 0), 255);
+    v[1] = a.cin == 3 ? min(max(s1 >> 22, 0), 255) : v[0];
+    v[2] = a.cin == 3 ? min(max(s2 >> 22, 0), 255) : v[0];
   }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) out[(long)c * per] = ((float)v[c] / 255.f - a.m[c]) / a.sd[c];
 }
 
 }  // namespace
@@ -232,6 +261,13 @@ extern "C" int dfk_mel_image(const float* wave, int64_t B, int64_t S, const floa
   if (r) return r;
   hipLaunchKernelGGL(mel_power_kernel, dim3((unsigned)T, (unsigned)B), dim3(256), 4 * nbin, s, X, ldx, (int)nbin,
                      (int)T, fbank, n_mels, Sm);
+  static bool lds_attr = false;   // the uint8 image may take up to 160 KB of dynamic LDS (clips past ~12 s)
+  if (!lds_attr) {
+    // (160 KB minus the kernel's static reduction scratch: the attribute counts dynamic LDS only)
+    (void)hipFuncSetAttribute((const void*)mel_image_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 256);
+    lds_attr = true;
+  }
   hipLaunchKernelGGL(mel_image_kernel, dim3((unsigned)B), dim3(1024), (size_t)n_mels * T, s, Sm, n_mels, (int)T,
                      out_h, out_w, out);
   DFK_CHECK_LAUNCH();
@@ -249,17 +285,23 @@ extern "C" int dfk_gray_normalize(const uint8_t* src, float* dst, int64_t n_img,
   return 0;
 }
 
-extern "C" int dfk_frame_augment(const uint8_t* src, int64_t frames, int32_t H, int32_t W, int32_t out_h,
-                                 int32_t out_w, const int32_t* flips, const float* angles, const float* mean3,
-                                 const float* std3, float* dst, hipStream_t s) {
-  if (!src || !dst || !mean3 || !std3 || H <= 0 || W <= 0 || out_h <= 0 || out_w <= 0) return DFK_EINVAL;
+extern "C" int dfk_frame_augment(const uint8_t* src, int64_t frames, const dfk_pil_resize* rs, const int32_t* flips,
+                                 const int32_t* affine, const float* mean3, const float* std3, uint8_t* tmp, float* dst,
+                                 hipStream_t s) {
+  if (!src || !rs || !dst || !tmp || !mean3 || !std3) return DFK_EINVAL;
+  const dfk_pil_resize& r = *rs;
+  if (r.H <= 0 || r.W <= 0 || r.out_h <= 0 || r.out_w <= 0 || (r.cin != 1 && r.cin != 3)) return DFK_EINVAL;
+  if (!r.xb || !r.xk || !r.yb || !r.yk || r.kx <= 0 || r.ky <= 0) return DFK_EINVAL;
   if (frames <= 0) return 0;
-  AugArgs a;
-  a.H = H; a.W = W; a.oh = out_h; a.ow = out_w;
+  PilArgs a;
+  a.H = r.H; a.W = r.W; a.cin = r.cin; a.oh = r.out_h; a.ow = r.out_w; a.kx = r.kx; a.ky = r.ky;
   for (int c = 0; c < 3; ++c) { a.m[c] = mean3[c]; a.sd[c] = std3[c]; }
-  const long n = frames * (long)out_h * out_w;
-  hipLaunchKernelGGL(frame_augment_kernel, dim3((unsigned)dfk_cdiv(n, 256)), dim3(256), 0, s, src, (long)frames, a,
-                     flips, angles, dst);
+  const long nw = frames * (long)r.H * r.out_w;
+  hipLaunchKernelGGL(pil_resize_w_kernel, dim3((unsigned)dfk_cdiv(nw, 256)), dim3(256), 0, s, src, (long)frames, a,
+                     r.xb, r.xk, tmp);
+  const long n = frames * (long)r.out_h * r.out_w;
+  hipLaunchKernelGGL(pil_augment_kernel, dim3((unsigned)dfk_cdiv(n, 256)), dim3(256), 0, s, tmp, (long)frames, a,
+                     r.yb, r.yk, flips, affine, dst);
   DFK_CHECK_LAUNCH();
   return 0;
 }

@@ -16,6 +16,21 @@
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// This file is built with IEEE mode off and no-NaN semantics (build.py FILE_FLAGS).  The device library's ockl
+// functions behind threadIdx / blockIdx / blockDim / gridDim / __umulhi carry the default attributes, so hipcc does
+// not inline them here: each use compiled to an s_swappc call (346 in this object, inside the K / V / Q gather
+// loops of every attention kernel).  These builtins are the inline instructions / dispatch-packet reads instead.
+__device__ __forceinline__ int dfk_tid() { return (int)__builtin_amdgcn_workitem_id_x(); }
+__device__ __forceinline__ int dfk_bid_x() { return (int)__builtin_amdgcn_workgroup_id_x(); }
+__device__ __forceinline__ int dfk_bid_y() { return (int)__builtin_amdgcn_workgroup_id_y(); }
+__device__ __forceinline__ int dfk_bid_z() { return (int)__builtin_amdgcn_workgroup_id_z(); }
+__device__ __forceinline__ int dfk_bdim() { return (int)__builtin_amdgcn_workgroup_size_x(); }
+__device__ __forceinline__ int dfk_gdim_x() {
+  const unsigned w = __builtin_amdgcn_workgroup_size_x();
+  return (int)((__builtin_amdgcn_grid_size_x() + w - 1) / w);
+}
+__device__ __forceinline__ uint32_t dfk_umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 struct TokInfo {
@@ -37,7 +52,7 @@ struct Geo {
 
 // floor(x / n) for x < 2^16, n < 2^16 with m = floor((2^32-1)/n) + 1 (m = 0 encodes n = 1): the error of
 // x*m/2^32 is below x/2^32 < 1/n, so the floor is exact; one v_mul_hi_u32 instead of a division sequence
-__device__ __forceinline__ int fdiv16(int x, uint32_t m) { return m ? (int)__umulhi((uint32_t)x, m) : x; }
+__device__ __forceinline__ int fdiv16(int x, uint32_t m) { return m ? (int)dfk_umulhi((uint32_t)x, m) : x; }
 
 __device__ __forceinline__ int region(int p, int P, int w, int s) {
   if (s == 0) return 2;
@@ -168,8 +183,8 @@ __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, 
   T* Vs = Ks + g.Np * HD;
   const int VTS = g.Np + 8;  // bf16 transposed-V row stride
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int unit = blockIdx.x;
+  const int tid = dfk_tid(), lane = tid & 63, wave = tid >> 6;
+  int unit = dfk_bid_x();
   const int head = unit % a.heads;
   unit /= a.heads;
   const int win = unit % g.nW, b = unit / g.nW;
@@ -200,7 +215,7 @@ __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, 
   const int grp = lane >> 4, ql = lane & 15;
   const int nqt = (g.N + 15) / 16;
   const int nkb = g.Np / 32;
-  for (int qt = blockIdx.y * 4 + wave; qt < nqt; qt += 4 * qsplit) {
+  for (int qt = dfk_bid_y() * 4 + wave; qt < nqt; qt += 4 * qsplit) {
     const int q = qt * 16 + ql;
     const TokInfo tq = q < g.N ? tok[q] : TokInfo{-2, 0, -1};
     // Q fragment (B operand: lane holds Q[q][e-slots])
@@ -341,7 +356,7 @@ __global__ __launch_bounds__(256) void wattn_fwd_kernel(const dfk_wattn_args a, 
         }
       }
     }
-    if (a.lse && grp == 0 && q < g.N) a.lse[((long)blockIdx.x) * g.Np + q] = m + __logf(l);
+    if (a.lse && grp == 0 && q < g.N) a.lse[((long)dfk_bid_x()) * g.Np + q] = m + __logf(l);
   }
 }
 
@@ -365,9 +380,9 @@ __global__ __launch_bounds__(256) void wattn_fwd_bf16_kernel(const dfk_wattn_arg
   bf16raw* Ks = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)g.Np * HD;
   bf16raw* Vs = reinterpret_cast<bf16raw*>(p);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = dfk_tid(), lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, ql = lane & 15, tq = ql >> 2, tp = ql & 3;
-  int unit = blockIdx.x;
+  int unit = dfk_bid_x();
   const int head = unit % a.heads;
   unit /= a.heads;
   const int win = unit % g.nW, b = unit / g.nW;
@@ -376,7 +391,7 @@ __global__ __launch_bounds__(256) void wattn_fwd_bf16_kernel(const dfk_wattn_arg
   if (tid == 0) mixed = 0;
   __syncthreads();
   int lab0 = -1;
-  for (int i = tid; i < g.Np; i += blockDim.x) {
+  for (int i = tid; i < g.Np; i += dfk_bdim()) {
     const TokInfo t = token_info(a, g, b, win, i);
     tpk[i] = (t.pos << 5) | (t.row == -2 ? 31 : t.lab);
     if (t.row != -2) {
@@ -386,10 +401,10 @@ __global__ __launch_bounds__(256) void wattn_fwd_bf16_kernel(const dfk_wattn_arg
   }
   if (g.use_mask && lab0 >= 0 && lab0 != token_info(a, g, b, win, 0).lab) mixed = 1;
   if (RPB)
-    for (int l = tid; l < g.L; l += blockDim.x) rpb2[l] = a.rpb[(long)l * a.heads + head] * kLog2e;
+    for (int l = tid; l < g.L; l += dfk_bdim()) rpb2[l] = a.rpb[(long)l * a.heads + head] * kLog2e;
   __syncthreads();
   constexpr int CH = HD / 8;
-  for (int idx = tid; idx < g.Np * CH; idx += blockDim.x) {
+  for (int idx = tid; idx < g.Np * CH; idx += dfk_bdim()) {
     const int i = idx / CH, c = (idx % CH) * 8;
     const int row = token_info_row(a, g, b, win, i);
     *reinterpret_cast<uint4*>(Ks + swz<HD>(i, c)) = tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + c);
@@ -404,8 +419,8 @@ __global__ __launch_bounds__(256) void wattn_fwd_bf16_kernel(const dfk_wattn_arg
   bf16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
-  const int nw = blockDim.x >> 6;
-  for (int qb = blockIdx.y * nw + wave; qb < nqb; qb += nw * qsplit) {
+  const int nw = dfk_bdim() >> 6;
+  for (int qb = dfk_bid_y() * nw + wave; qb < nqb; qb += nw * qsplit) {
     // the lane's queries (one per 16-query half) and their Q^T B operands
     int qpk[2], qrow[2];
     bf16x8 qf[2][HD / 32];
@@ -528,7 +543,7 @@ __global__ __launch_bounds__(256) void wattn_fwd_bf16_kernel(const dfk_wattn_arg
           *reinterpret_cast<uint2*>(op + et * 16 + grp * 4) = u;
         }
       }
-      if (a.lse && grp == 0 && q < g.N) a.lse[((long)blockIdx.x) * g.Np + q] = (m[qh] + __log2f(l)) * 0.6931471805599453f;
+      if (a.lse && grp == 0 && q < g.N) a.lse[((long)dfk_bid_x()) * g.Np + q] = (m[qh] + __log2f(l)) * 0.6931471805599453f;
     }
   }
 }
@@ -598,7 +613,7 @@ struct WUnit {
 };
 
 __device__ __forceinline__ WUnit decode_unit(const dfk_wattn_args& a, const Geo& g, int qsplit) {
-  const int total = gridDim.x, bid = blockIdx.x;
+  const int total = dfk_gdim_x(), bid = dfk_bid_x();
   const int xcd = bid & 7, per = total >> 3, rr = total & 7;
   int u = (xcd < rr ? xcd * (per + 1) : rr * (per + 1) + (xcd - rr) * per) + (bid >> 3);
   WUnit w;
@@ -643,11 +658,12 @@ __device__ __forceinline__ float grp_max4(float v) {
 // Score bias in log2 units, bf16, in the operand order of the MFMA that adds it:
 //   bias'(q, k) = (rpb[pos(q) - pos(k) + C0] + (label(q) != label(k) ? -100 : 0)) * log2(e),
 //   -1e4 for keys >= N (finite: the identity product below must never meet an infinity), 0 for queries >= N.
-// A 32x32 score tile gets its bias from two v_mfma_f32_32x32x16_bf16 products bias_c x I_c (c = query half):
-// I_c[slot][n] = (slot == n - 16c) is a constant identity operand, so the add costs two MFMA issues and
-// no VALU, and the tile streams as 2 KB of bf16 instead of 4 KB of fp32.
-//   fwd layout (S^T: key on the row, query on the lane) [cls][head][qb][kb][c][64 lanes][8]:
-//       lane l, element j <-> k = 32 kb + (l & 31), q = 32 qb + 16 c + 8 (l >> 5) + j
+// The tile streams as 2 KB of bf16 (4 KB as fp32).  The forward adds it through the C input of the first QK^T
+// MFMA (unpacked to fp32 on the VALU, with -m folded in), so its layout is the S^T accumulator's; the backward
+// adds it with two v_mfma_f32_32x32x16_bf16 products bias_c x I_c (I_c[slot][n] = (slot == n - 16c), a constant
+// identity operand), so its layout is that product's A operand:
+//   fwd layout (S^T accumulator: key on the row, query on the lane) [cls][head][qb][kb][c][64 lanes][8]:
+//       lane l, element jj, j = 8 c + jj <-> q = 32 qb + (l & 31), k = 32 kb + (j & 3) + 8 (j >> 2) + 4 (l >> 5)
 //   bwd layout (S: query on the row, key on the lane)  [cls][head][qb][kb][c][64 lanes][8]:
 //       lane l, element j <-> q = 32 qb + (l & 31), k = 32 kb + 16 c + 8 (l >> 5) + j
 constexpr float kPadKey = -1.0e4f;
@@ -657,10 +673,10 @@ __global__ __launch_bounds__(256) void wattn_tab3_kernel(const dfk_wattn_args a,
   extern __shared__ int tsm[];
   int* tok = tsm;                                          // [Np]
   float* rp = reinterpret_cast<float*>(tsm + g.Np);        // [L]
-  const int ch = blockIdx.y, h = ch % a.heads, cls = ch / a.heads;
+  const int ch = dfk_bid_y(), h = ch % a.heads, cls = ch / a.heads;
   const float pen = -100.f * kLog2e;
-  for (int i = threadIdx.x; i < g.Np; i += blockDim.x) tok[i] = i < g.N ? tab_token(a, i) : 0;
-  for (int l = threadIdx.x; l < g.L; l += blockDim.x) rp[l] = a.rpb ? a.rpb[(long)l * a.heads + h] * kLog2e : 0.f;
+  for (int i = dfk_tid(); i < g.Np; i += dfk_bdim()) tok[i] = i < g.N ? tab_token(a, i) : 0;
+  for (int l = dfk_tid(); l < g.L; l += dfk_bdim()) rp[l] = a.rpb ? a.rpb[(long)l * a.heads + h] * kLog2e : 0.f;
   __syncthreads();
   auto val = [&](int q, int k) -> float {
     if (k >= g.N) return kPadKey;
@@ -672,7 +688,7 @@ __global__ __launch_bounds__(256) void wattn_tab3_kernel(const dfk_wattn_args a,
   };
   const int nkb = g.Np / 32;
   const long slots = (long)g.Np * g.Np / 8;   // 16-B slots per layout per (class, head)
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < 2 * slots; t += (long)gridDim.x * blockDim.x) {
+  for (long t = (long)dfk_bid_x() * dfk_bdim() + dfk_tid(); t < 2 * slots; t += (long)dfk_gdim_x() * dfk_bdim()) {
     const bool bwd = t >= slots;
     const long u = bwd ? t - slots : t;
     const int lane = (int)(u & 63), c = (int)((u >> 6) & 1);
@@ -685,8 +701,9 @@ __global__ __launch_bounds__(256) void wattn_tab3_kernel(const dfk_wattn_args a,
     for (int j = 0; j < 8; j += 2) {
       float v0, v1;
       if (!bwd) {
-        v0 = val(qb * 32 + 16 * c + 8 * hh + j, kb * 32 + rr);
-        v1 = val(qb * 32 + 16 * c + 8 * hh + j + 1, kb * 32 + rr);
+        const int j0 = 8 * c + j, j1 = j0 + 1;
+        v0 = val(qb * 32 + rr, kb * 32 + (j0 & 3) + 8 * (j0 >> 2) + 4 * hh);
+        v1 = val(qb * 32 + rr, kb * 32 + (j1 & 3) + 8 * (j1 >> 2) + 4 * hh);
       } else {
         v0 = val(qb * 32 + rr, kb * 32 + 16 * c + 8 * hh + j);
         v1 = val(qb * 32 + rr, kb * 32 + 16 * c + 8 * hh + j + 1);
@@ -747,7 +764,7 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16raw* Ks = reinterpret_cast<bf16raw*>(smem);
   bf16raw* Vs = Ks + (size_t)g.Np * HD;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tid = dfk_tid(), lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const WUnit wu = decode_unit(a, g, qsplit);
   const int head = wu.head, win = wu.win, b = wu.b;
@@ -759,12 +776,12 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
   {
     constexpr int KV_B = 4;
     const int tot = g.Np * CH;
-    for (int base = tid; base < tot; base += KV_B * blockDim.x) {
+    for (int base = tid; base < tot; base += KV_B * dfk_bdim()) {
       uint4 kv[KV_B], vv[KV_B];
       int off[KV_B];
 #pragma unroll
       for (int u = 0; u < KV_B; ++u) {
-        const int idx = min(base + u * (int)blockDim.x, tot - 1);
+        const int idx = min(base + u * (int)dfk_bdim(), tot - 1);
         const int i = idx / CH, c = (idx % CH) * 8;
         const int row = token_info_row(a, g, b, win, i);
         off[u] = swz<HD>(i, c);
@@ -773,7 +790,7 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
       }
 #pragma unroll
       for (int u = 0; u < KV_B; ++u) {
-        if (base + u * (int)blockDim.x < tot) {
+        if (base + u * (int)dfk_bdim() < tot) {
           *reinterpret_cast<uint4*>(Ks + off[u]) = kv[u];
           *reinterpret_cast<uint4*>(Vs + off[u]) = vv[u];
         }
@@ -788,7 +805,7 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
   const DropCtx dc = drop_ctx(a.drop);
   __syncthreads();
 
-  const int nw = blockDim.x >> 6, qstep = nw * qsplit;
+  const int nw = dfk_bdim() >> 6, qstep = nw * qsplit;
   int qrown;
   bf16x8 qfn[NKK];
   auto load_q = [&](int qb) {   // Q'^T B operands of query 32 qb + r: elements 8 hh + j of each 16-wide k-step
@@ -943,6 +960,244 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd3_k
   }
 }
 
+// Forward v4 (bias tables): v3's structure with the score bias entering as the C input of the first QK^T MFMA and
+// the softmax denominator summed on the VALU — per 32x32 block the matrix pipe runs only the 4 algorithmic
+// 32x32x16 products (v3: 8 MFMA-equivalents: the -m k-step, two identity-operand bias products and the selector
+// row sums besides them, and the bias products sat on the chain QK^T -> bias -> max).  The bias tile arrives one
+// block ahead (buffer loads, accumulator order: 2 x 16 B per lane) and is unpacked to fp32 minus m off the chain.
+// QB query blocks per wave (2 for hd 32): each key block's K / V fragments are read from LDS once for both, and
+// the two independent score -> softmax -> PV chains interleave (the kernel is latency-bound, not MFMA-bound:
+// r4f ablations, profiles/attn/r4f_fwd4_ablations.txt).
+// Lane l holds query 32 qb + (l & 31) and keys (j & 3) + 8 (j >> 2) + 4 (l >> 5) of every tile; lanes l and l ^ 32
+// hold the two key halves of one query, so the per-lane partial sums meet in one permlane32 swap at the end.
+template <int HD, bool DROP, int QB>
+__global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd4_kernel(const dfk_wattn_args a, const Geo g, int qsplit,
+                                                         const bf16raw* __restrict__ tab) {
+  constexpr int NKK = HD / 16, NOT = HD / 32, CH = HD / 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16raw* Ks = reinterpret_cast<bf16raw*>(smem);
+  bf16raw* Vs = Ks + (size_t)g.Np * HD;
+  const int tid = dfk_tid(), lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  const WUnit wu = decode_unit(a, g, qsplit);
+  const int head = wu.head, win = wu.win, b = wu.b;
+  const long unit = wu.lse_unit;
+  const int hoff = head * HD;
+  {   // K / V gather, KV_B chunks per thread in flight (as v3)
+    constexpr int KV_B = 4;
+    const int tot = g.Np * CH;
+    for (int base = tid; base < tot; base += KV_B * dfk_bdim()) {
+      uint4 kv[KV_B], vv[KV_B];
+      int off[KV_B];
+#pragma unroll
+      for (int u = 0; u < KV_B; ++u) {
+        const int idx = min(base + u * (int)dfk_bdim(), tot - 1);
+        const int i = idx / CH, c = (idx % CH) * 8;
+        const int row = token_info_row(a, g, b, win, i);
+        off[u] = swz<HD>(i, c);
+#ifdef DFK_ABL_NOGATHER
+        kv[u] = make_uint4(row, c, 0, 0); vv[u] = kv[u];
+#else
+        kv[u] = tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + c);
+        vv[u] = tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + c);
+#endif
+      }
+#pragma unroll
+      for (int u = 0; u < KV_B; ++u) {
+        if (base + u * (int)dfk_bdim() < tot) {
+          *reinterpret_cast<uint4*>(Ks + off[u]) = kv[u];
+          *reinterpret_cast<uint4*>(Vs + off[u]) = vv[u];
+        }
+      }
+    }
+  }
+  const int nkb = g.Np / 32, nqb = g.Np / 32, ngrp = (nqb + QB - 1) / QB;
+  const bf16raw* tch = tab + ((long)wu.cls * a.heads + head) * (long)g.Np * g.Np;
+  const float qs = a.scale * kLog2e;
+  const DropCtx dc = drop_ctx(a.drop);
+  __syncthreads();
+
+  const int nw = dfk_bdim() >> 6, qstep = nw * qsplit;
+  int qrown[QB];
+  bf16x8 qfn[QB][NKK];
+  // query group gi = query blocks QB gi .. QB gi + QB - 1 (clamped: a group past the last block recomputes it
+  // and stores nothing)
+  auto load_q = [&](int gi) {
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      const int q = min(gi * QB + u, nqb - 1) * 32 + r;
+      qrown[u] = q < g.N ? token_info_row(a, g, b, win, q) : -2;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk)
+        qfn[u][kk] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.q, a.pad_q, qrown[u], a.ld_qkv, hoff + kk * 16 + hh * 8));
+    }
+  };
+  int koff[NKK], vlo[NOT], vhi[NOT];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) koff[kk] = swz<HD>(r, kk * 16 + hh * 8);
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot) {
+    const int k0 = 4 * (g16 >> 1) + tq, col = ot * 32 + 16 * (g16 & 1) + 4 * tp;
+    vlo[ot] = swz<HD>(k0, col);
+    vhi[ot] = swz<HD>(k0 + 8, col);
+  }
+  const uint64_t tp64 = reinterpret_cast<uint64_t>(tch);
+  const uint64_t tpu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tp64 >> 32)) << 32) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tp64);
+  const __amdgpu_buffer_rsrc_t trs =
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(tpu), (short)0, 0x7fffffff, 0x00020000);
+  // QB == 1: the next group's Q is prefetched under this group's blocks; QB == 2 loads it at the group's start
+  // (the 16 prefetch VGPRs would push the two-chain kernel past the 3-workgroup register budget)
+  if constexpr (QB == 1) load_q(min(wu.qpart * nw + wave, ngrp - 1));
+#ifdef DFK_ABL_NOCOMPUTE
+  if (wave == -7)
+#endif
+  for (int gi = wu.qpart * nw + wave; gi < ngrp; gi += qstep) {
+    int qbs[QB], qrow[QB];
+    bf16x8 qf[QB][NKK];
+    if constexpr (QB > 1) load_q(gi);
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      qbs[u] = min(gi * QB + u, nqb - 1);
+      qrow[u] = gi * QB + u < nqb ? qrown[u] : -1;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[u][kk][j] = (__bf16)((float)qfn[u][kk][j] * qs);
+    }
+    if constexpr (QB == 1) load_q(min(gi + qstep, ngrp - 1));
+    auto load_bias = [&](uint4 (&bt)[QB][2], int kb) {
+#pragma unroll
+      for (int u = 0; u < QB; ++u) {
+        const int so = __builtin_amdgcn_readfirstlane((qbs[u] * nkb + kb) * 2048);   // bytes: 1024 bf16 per tile
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+#ifdef DFK_ABL_NOBIAS
+          bt[u][c] = make_uint4(so, c, 0, 0);
+#else
+          bt[u][c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(trs, lane * 16, so + c * 1024, 0));
+#endif
+        }
+      }
+    };
+    f32x16 o[QB][NOT];
+    float lsum[QB], m[QB];
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      lsum[u] = 0.f;
+      m[u] = 0.f;
+#pragma unroll
+      for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) o[u][ot][j] = 0.f;
+    }
+    uint4 bt[QB][2];
+    load_bias(bt, 0);
+    for (int kb = 0; kb < nkb; ++kb) {
+      const bf16raw* kbase = Ks + kb * 32 * HD;
+      const bf16raw* vbase = Vs + kb * 32 * HD;
+      bf16x8 kf[NKK];
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) kf[kk] = *reinterpret_cast<const bf16x8*>(kbase + koff[kk]);
+      // C input: bias' - m (bf16 pairs unpacked by shift / mask), then D = K Q'^T + bias' - m
+      f32x16 d[QB];
+#pragma unroll
+      for (int u = 0; u < QB; ++u)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const uint32_t w[4] = {bt[u][c].x, bt[u][c].y, bt[u][c].z, bt[u][c].w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            d[u][8 * c + 2 * i] = __uint_as_float(w[i] << 16) - m[u];
+            d[u][8 * c + 2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u) - m[u];
+          }
+        }
+      load_bias(bt, min(kb + 1, nkb - 1));   // next block's tiles: in flight under this block's softmax and PV
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk)
+#pragma unroll
+        for (int u = 0; u < QB; ++u) d[u] = mfma32(kf[kk], qf[u][kk], d[u]);
+      bf16x8 va[2][NOT];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot) va[c][ot] = tr16x2(vbase + c * 16 * HD + vlo[ot], vbase + c * 16 * HD + vhi[ot]);
+      bf16x8 pv[QB][2];
+#pragma unroll
+      for (int u = 0; u < QB; ++u) {
+        float x0 = max3f(d[u][0], d[u][1], d[u][2]), x1 = max3f(d[u][3], d[u][4], d[u][5]);
+        float x2 = max3f(d[u][6], d[u][7], d[u][8]), x3 = max3f(d[u][9], d[u][10], d[u][11]);
+        float x4 = max3f(d[u][12], d[u][13], d[u][14]);
+        float bm = max3f(max3f(x0, x1, x2), max3f(x3, x4, d[u][15]), -INFINITY);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(bm), __float_as_uint(bm), false, false);
+        bm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        const bool grow = kb == 0 || bm > kRescale;
+        if (__builtin_amdgcn_ballot_w64(grow) != 0) {
+          const float mn = grow ? bf16_ceil(m[u] + bm) : m[u];
+          const float delta = mn - m[u];
+          const float alpha = kb == 0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
+          m[u] = mn;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) d[u][j] -= delta;
+          lsum[u] *= alpha;
+#pragma unroll
+          for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) o[u][ot][j] *= alpha;
+        }
+        // P = 2^D as the B operand of k-steps c = 0, 1 (registers 8c .. 8c+7); the denominator sums fp32 P
+        float p[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+#ifdef DFK_ABL_NOEXP
+          p[j] = d[u][j];
+#else
+          p[j] = __builtin_amdgcn_exp2f(d[u][j]);
+#endif
+        }
+        const float s0 = (p[0] + p[1]) + (p[2] + p[3]), s1 = (p[4] + p[5]) + (p[6] + p[7]);
+        const float s2 = (p[8] + p[9]) + (p[10] + p[11]), s3 = (p[12] + p[13]) + (p[14] + p[15]);
+        lsum[u] += (s0 + s1) + (s2 + s3);
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float pj = p[8 * c + j];
+            if constexpr (DROP)   // O accumulates the dropped probabilities, the denominator the undropped ones
+              pj *= drop_mul(dc, unit * g.Np + qbs[u] * 32 + r, kb * 32 + 16 * c + 8 * (j >> 2) + 4 * hh + (j & 3));
+            pv[u][c][j] = (__bf16)pj;
+          }
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+          for (int u = 0; u < QB; ++u) o[u][ot] = mfma32(va[c][ot], pv[u][c], o[u][ot]);
+    }
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      const auto ls = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum[u]), __float_as_uint(lsum[u]), false, false);
+      const float l = __uint_as_float(ls[0]) + __uint_as_float(ls[1]);
+      const float inv = 1.f / l;
+      if (qrow[u] >= 0) {
+        bf16raw* op = reinterpret_cast<bf16raw*>(a.out) + (long)qrow[u] * a.ld_out + hoff;
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+          for (int jg = 0; jg < 4; ++jg) {
+            uint2 w;
+            w.x = (uint32_t)f2bf(o[u][ot][4 * jg] * inv) | ((uint32_t)f2bf(o[u][ot][4 * jg + 1] * inv) << 16);
+            w.y = (uint32_t)f2bf(o[u][ot][4 * jg + 2] * inv) | ((uint32_t)f2bf(o[u][ot][4 * jg + 3] * inv) << 16);
+            *reinterpret_cast<uint2*>(op + ot * 32 + 8 * jg + 4 * hh) = w;
+          }
+      }
+      const int q = qbs[u] * 32 + r;
+      if (a.lse && hh == 0 && q < g.N && gi * QB + u < nqb) a.lse[unit * g.Np + q] = (m[u] + __log2f(l)) * 0.6931471805599453f;
+    }
+  }
+}
+
 size_t fwd_lds_bf16(const dfk_wattn_args& a, const Geo& g) {
   return 16 + 4 * (size_t)g.Np + 4 * (size_t)((g.L + 3) & ~3) + 4 * (size_t)g.Np * a.hd;
 }
@@ -1013,12 +1268,16 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     const size_t lds = 4 * (size_t)g.Np * a.hd;
     if (lds > 160 * 1024) return DFK_EINVAL;
     const int nqb = g.Np / 32;
-    const int nw = std::min(4, nqb);
-    const int qsplit = (int)std::max<long>(1, std::min<long>(dfk_cdiv(nqb, nw), dfk_cdiv(1024, units)));
+    // query blocks per wave: 2 for the hd-32 table kernel (K / V fragment reads shared, two chains interleaved)
+    static const int qgrp_env = getenv("DFK_WATTN_QB") ? atoi(getenv("DFK_WATTN_QB")) : 2;   // A/B runs only
+    const int qgrp = tab && a.hd == 32 && !a.drop.mode && nqb >= 2 ? qgrp_env : 1;
+    const int ngrp = dfk_cdiv(nqb, qgrp);
+    const int nw = std::min(4, ngrp);
+    const int qsplit = (int)std::max<long>(1, std::min<long>(dfk_cdiv(ngrp, nw), dfk_cdiv(1024, units)));
     dim3 grid((unsigned)(units * qsplit));
-#define LAUNCH_3(HD, TB, DR)                                                                                 \
+#define LAUNCH_K(KFN)                                                                                        \
   do {                                                                                                       \
-    auto kfn = wattn_fwd3_kernel<HD, TB, DR>;                                                                \
+    auto kfn = KFN;                                                                                          \
     static bool attr_set = false;                                                                            \
     if (!attr_set) {                                                                                         \
       (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);   \
@@ -1026,14 +1285,23 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     }                                                                                                        \
     hipLaunchKernelGGL(kfn, grid, dim3(64 * nw), lds, s, a, g, qsplit, t3);                                 \
   } while (0)
-#define PICK_3(HD)                                                                       \
-  do {                                                                                   \
-    if (tab) { if (a.drop.mode) LAUNCH_3(HD, true, true); else LAUNCH_3(HD, true, false); } \
-    else { if (a.drop.mode) LAUNCH_3(HD, false, true); else LAUNCH_3(HD, false, false); }   \
-  } while (0)
-    if (a.hd == 32) PICK_3(32); else PICK_3(64);
-#undef PICK_3
-#undef LAUNCH_3
+    // bias tables: v4 (bias through the QK^T C input, VALU row sums); no bias: v3's table-free form
+    if (a.hd == 32) {
+      if (tab) {
+        if (a.drop.mode) LAUNCH_K((wattn_fwd4_kernel<32, true, 1>));
+        else if (qgrp == 2) LAUNCH_K((wattn_fwd4_kernel<32, false, 2>));
+        else LAUNCH_K((wattn_fwd4_kernel<32, false, 1>));
+      } else {
+        if (a.drop.mode) LAUNCH_K((wattn_fwd3_kernel<32, false, true>)); else LAUNCH_K((wattn_fwd3_kernel<32, false, false>));
+      }
+    } else {
+      if (tab) {
+        if (a.drop.mode) LAUNCH_K((wattn_fwd4_kernel<64, true, 1>)); else LAUNCH_K((wattn_fwd4_kernel<64, false, 1>));
+      } else {
+        if (a.drop.mode) LAUNCH_K((wattn_fwd3_kernel<64, false, true>)); else LAUNCH_K((wattn_fwd3_kernel<64, false, false>));
+      }
+    }
+#undef LAUNCH_K
     DFK_CHECK_LAUNCH();
     return 0;
   }
@@ -1105,7 +1373,7 @@ namespace {
 __device__ __forceinline__ void flush_drpb(const dfk_wattn_bwd_args& ba, const Geo& g, const float* drpb, int head,
                                            int accum, int tid, int nthreads) {
   if (ba.ws) {
-    float* w = ba.ws + (long)blockIdx.x * ((g.L + 3) & ~3);
+    float* w = ba.ws + (long)dfk_bid_x() * ((g.L + 3) & ~3);
     for (int l = tid; l < g.L; l += nthreads) w[l] = accum ? w[l] + drpb[l] : drpb[l];
   } else {
     for (int l = tid; l < g.L; l += nthreads)
@@ -1118,8 +1386,8 @@ __global__ __launch_bounds__(1024) void drpb_reduce_kernel(const float* __restri
                                                            float* __restrict__ drpb) {
   __shared__ float part[16][64];
   const int Lal = (L + 3) & ~3;
-  const int c = threadIdx.x & 63, ph = threadIdx.x >> 6, h = blockIdx.y;
-  const int l = blockIdx.x * 64 + c;
+  const int c = dfk_tid() & 63, ph = dfk_tid() >> 6, h = dfk_bid_y();
+  const int l = dfk_bid_x() * 64 + c;
   float s = 0.f;
   if (l < L)
     for (long u = h + (long)heads * ph; u < units; u += (long)heads * 16) s += ws[u * Lal + l];
@@ -1153,9 +1421,9 @@ __global__ __launch_bounds__(256) void wattn_bwd_kernel(const dfk_wattn_bwd_args
   T* dOs = reinterpret_cast<T*>(p); p += sizeof(T) * (size_t)Qn * HD;
   T* Sd = reinterpret_cast<T*>(p);  // 4 waves x [32 q][32 k]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = dfk_tid(), lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, ql = lane & 15;
-  int unit = blockIdx.x;
+  int unit = dfk_bid_x();
   const int head = unit % a.heads;
   unit /= a.heads;
   const int win = unit % g.nW, b = unit / g.nW;
@@ -1188,7 +1456,7 @@ __global__ __launch_bounds__(256) void wattn_bwd_kernel(const dfk_wattn_bwd_args
       for (int e = 0; e < HD; ++e) d += ldf<T>(op + e) * ldf<T>(dop + e);
     }
     delta[li] = d;
-    lse[li] = (i < g.N) ? a.lse[(long)blockIdx.x * g.Np + i] : 0.f;
+    lse[li] = (i < g.N) ? a.lse[(long)dfk_bid_x() * g.Np + i] : 0.f;
   }
   __syncthreads();
 
@@ -1420,7 +1688,7 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
   // dS^T also goes to global scratch (dsg) for the deterministic dRPB reduction.  No LDS atomics.
   const dfk_wattn_args& a = ba.f;
   constexpr int kDqStride = HD + 4;  // fp32 row stride of the per-wave dQ partials [32 queries][HD]
-  const int nwaves = blockDim.x >> 6;
+  const int nwaves = dfk_bdim() >> 6;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int Lal = (g.L + 3) & ~3;
   char* p = smem;
@@ -1434,9 +1702,9 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
   bf16raw* dOs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Qn * HD;
   bf16raw* Sd = reinterpret_cast<bf16raw*>(p);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = dfk_tid(), lane = tid & 63, wave = tid >> 6;
   const int grp = lane >> 4, ql = lane & 15, tq = ql >> 2, tp = ql & 3;
-  int unit = blockIdx.x;
+  int unit = dfk_bid_x();
   const int head = unit % a.heads;
   unit /= a.heads;
   const int win = unit % g.nW, b = unit / g.nW;
@@ -1446,21 +1714,21 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
   const bf16raw* dog = reinterpret_cast<const bf16raw*>(ba.dout);
   const bf16raw* qg = reinterpret_cast<const bf16raw*>(a.q);
 
-  for (int i = tid; i < g.Np; i += blockDim.x) {
+  for (int i = tid; i < g.Np; i += dfk_bdim()) {
     const TokInfo t = token_info(a, g, b, win, i);
     trow[i] = t.row;
     tpk[i] = (t.pos << 5) | (t.lab & 31);
   }
   if (RPB)
-    for (int l = tid; l < g.L; l += blockDim.x) rpb2[l] = a.rpb[(long)l * a.heads + head] * kLog2e;
-  for (int li = tid; li < Qn; li += blockDim.x) {
+    for (int l = tid; l < g.L; l += dfk_bdim()) rpb2[l] = a.rpb[(long)l * a.heads + head] * kLog2e;
+  for (int li = tid; li < Qn; li += dfk_bdim()) {
     const int i = q0 + li;
-    lse2[li] = i < g.N ? a.lse[(long)blockIdx.x * g.Np + i] * kLog2e : INFINITY;
+    lse2[li] = i < g.N ? a.lse[(long)dfk_bid_x() * g.Np + i] * kLog2e : INFINITY;
   }
   __syncthreads();
   // Q, dO rows -> swizzled LDS tiles; delta = rowsum(O * dO) (CH lanes per row)
   constexpr int CH = HD / 8;
-  for (int base = 0; base < Qn * CH; base += blockDim.x) {
+  for (int base = 0; base < Qn * CH; base += dfk_bdim()) {
     const int idx = base + tid;
     float d = 0.f;
     if (idx < Qn * CH) {
@@ -1486,7 +1754,7 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
   float* myQ = dQp + wave * 32 * kDqStride;
   const float scale2 = a.scale * kLog2e;
   const float mpen = -100.f * kLog2e;
-  bf16raw* dsu = RPB && dsg ? dsg + (long)blockIdx.x * g.Np * g.Np : nullptr;   // this window-head's dS^T [k][q]
+  bf16raw* dsu = RPB && dsg ? dsg + (long)dfk_bid_x() * g.Np * g.Np : nullptr;   // this window-head's dS^T [k][q]
   for (int pass = 0; pass * nwaves < nkb; ++pass) {
     const int kb = pass * nwaves + wave;
     const bool own = kb < nkb;
@@ -1634,7 +1902,7 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
           for (int r = 0; r < 4; ++r) myQ[(qh * 16 + grp * 4 + r) * kDqStride + et * 16 + ql] = dq[qh][et][r];
       __syncthreads();
       const int nw = min(nwaves, nkb - pass * nwaves);
-      for (int t = tid; t < 32 * (HD / 8); t += blockDim.x) {
+      for (int t = tid; t < 32 * (HD / 8); t += dfk_bdim()) {
         const int lr = t / (HD / 8), c = (t % (HD / 8)) * 8;
         float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         for (int w = 0; w < nw; ++w) {
@@ -1709,7 +1977,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
                                                          const bf16raw* __restrict__ tabb) {
   constexpr int NKK = HD / 16, NOT = HD / 32, CH = HD / 8;
   const dfk_wattn_args& a = ba.f;
-  const int nw = blockDim.x >> 6;
+  const int nw = dfk_bdim() >> 6;
   // queries [q0, q0 + Qn) of every window (Qn = Np unless the window's Q / dO / dQ do not fit the LDS: then
   // several launches, dK / dV accumulated in place by the later ones)
   const int Np = g.Np, nkb = Np / 32, nqb = Qn / 32;
@@ -1723,7 +1991,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   float* nl2 = reinterpret_cast<float*>(p); p += 4 * Qn;   // -lse log2e; -inf beyond N (P = 0)
   float* ndl = reinterpret_cast<float*>(p); p += 4 * Qn;   // -delta
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tid = dfk_tid(), lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const WUnit wu = decode_unit(a, g, 1);   // the forward's work order; lse / dS^T / dropout rows by lse_unit
   const int head = wu.head, win = wu.win, b = wu.b;
@@ -1738,21 +2006,21 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
       __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(tpu), (short)0, TAB ? 0x7fffffff : 0, 0x00020000);
   const float qs = a.scale * kLog2e;
 
-  for (int i = tid; i < Np; i += blockDim.x) trow[i] = token_info_row(a, g, b, win, i);
-  for (int i = tid; i < Qn; i += blockDim.x)
+  for (int i = tid; i < Np; i += dfk_bdim()) trow[i] = token_info_row(a, g, b, win, i);
+  for (int i = tid; i < Qn; i += dfk_bdim())
     nl2[i] = q0 + i < g.N ? -a.lse[unit * Np + q0 + i] * kLog2e : -INFINITY;
-  for (int i = tid * 4; i < Qn * HD; i += blockDim.x * 4) *reinterpret_cast<f32x4*>(dQa + i) = f32x4{0, 0, 0, 0};
+  for (int i = tid * 4; i < Qn * HD; i += dfk_bdim() * 4) *reinterpret_cast<f32x4*>(dQa + i) = f32x4{0, 0, 0, 0};
   __syncthreads();
   // Q / dO / O gather, QB row chunks per thread in flight (all loads of a batch issued before the wait that
   // precedes their use: one HBM round trip per batch, not per chunk)
   {
     constexpr int QB = 4;
     const int tot = Qn * CH;
-    for (int base = 0; base < tot; base += QB * blockDim.x) {
+    for (int base = 0; base < tot; base += QB * dfk_bdim()) {
       uint4 qv[QB], dv[QB], ov[QB];
 #pragma unroll
       for (int u = 0; u < QB; ++u) {
-        const int idx = min(base + u * (int)blockDim.x + tid, tot - 1);
+        const int idx = min(base + u * (int)dfk_bdim() + tid, tot - 1);
         const int li = idx / CH, c = (idx % CH) * 8;
         const int row = trow[q0 + li];
         qv[u] = tok_ld16<bf16raw>(a.q, a.pad_q, row, a.ld_qkv, hoff + c);
@@ -1761,7 +2029,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
       }
 #pragma unroll
       for (int u = 0; u < QB; ++u) {
-        const int idx = base + u * (int)blockDim.x + tid;   // CH | blockDim: a row's CH lanes agree on idx < tot
+        const int idx = base + u * (int)dfk_bdim() + tid;   // CH | blockDim: a row's CH lanes agree on idx < tot
         float d = dot8_bf16(ov[u], dv[u]);
 #pragma unroll
         for (int o = 1; o < CH; o <<= 1) d += __shfl_xor(d, o, 64);
@@ -1969,7 +2237,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   }
   __syncthreads();
   // dQ rows (scaled): (q, e) of block qb sits at [qb][ot][v][lane][t], q = 32 qb + 8 v + 4 h + t, lane = (e & 31) + 32 h
-  for (int t8 = tid; t8 < Qn * (HD / 8); t8 += blockDim.x) {
+  for (int t8 = tid; t8 < Qn * (HD / 8); t8 += dfk_bdim()) {
     const int i = t8 / (HD / 8), c = (t8 % (HD / 8)) * 8;
     const int row = q0 + i < g.N ? trow[q0 + i] : -2;
     const int qb = i >> 5, qi = i & 31, v = qi >> 3, h2 = (qi >> 2) & 1, t = qi & 3, ot = c >> 5;
@@ -2001,11 +2269,11 @@ __global__ __launch_bounds__(256) void drpb_from_ds_kernel(const bf16raw* __rest
                                                            int Np, int N, int fh, int fw, int C0, int L, int wps,
                                                            float* __restrict__ rows) {
   extern __shared__ float tab[];
-  const int chunk = blockIdx.x, h = blockIdx.y, split = blockIdx.z;
+  const int chunk = dfk_bid_x(), h = dfk_bid_y(), split = dfk_bid_z();
   const int Lal = (L + 3) & ~3;
-  for (int l = threadIdx.x; l < L; l += blockDim.x) tab[l] = 0.f;
+  for (int l = dfk_tid(); l < L; l += dfk_bdim()) tab[l] = 0.f;
   __syncthreads();
-  const long e0 = ((long)chunk * blockDim.x + threadIdx.x) * 8;
+  const long e0 = ((long)chunk * dfk_bdim() + dfk_tid()) * 8;
   const long NN = (long)Np * Np;
   if (e0 < NN) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -2041,8 +2309,8 @@ __global__ __launch_bounds__(256) void drpb_from_ds_kernel(const bf16raw* __rest
     }
   }
   __syncthreads();
-  float* row = rows + ((long)(split * gridDim.x + chunk) * heads + h) * Lal;
-  for (int l = threadIdx.x; l < L; l += blockDim.x) row[l] = tab[l];
+  float* row = rows + ((long)(split * dfk_gdim_x() + chunk) * heads + h) * Lal;
+  for (int l = dfk_tid(); l < L; l += dfk_bdim()) row[l] = tab[l];
 }
 
 struct DsPlan {

@@ -6,10 +6,11 @@ The constants the kernels read — the window-folded DFT basis of librosa's STFT
 Slaney mel filterbank — are built here once per (sr, n_fft, n_mels) in float64 and cast to
 float32, as librosa does; they are parameters of the transform, not data.
 
-Parity: librosa, cv2 and PIL are not importable in this image, so the mel image and the
-augmentation are pinned to the restatement in oracle/media.py (librosa 0.10 / OpenCV 4 /
-torchvision semantics restated from their published algorithms) — parity unpinned against
-the libraries themselves."""
+Parity: the frame / mel-image transform follows PIL 12.2 (importable here), as the reference applies
+torchvision's transforms to PIL images: pinned bit for bit to PIL fixtures (tests/golden/pil_frames.npz, written
+by tests/golden/make_pil_fixtures.py).  librosa and cv2 are absent, so the mel-spectrogram image stays pinned to
+the restatement in oracle/media.py (librosa 0.10 / OpenCV 4 semantics from their published algorithms) — parity
+unpinned against those libraries."""
 import ctypes
 import functools
 import math
@@ -116,32 +117,118 @@ def gray_normalize(img_u8, mean=IMAGENET_MEAN, std=IMAGENET_STD):
     return out
 
 
-def draw_augment(frames, device, generator=None, degrees=90.0):
-    """Per-frame random parameters of RandomHorizontalFlip / RandomVerticalFlip (p = 0.5) and
-    RandomRotation(degrees) (uniform angle in [-degrees, degrees]): (flips int32 [frames], angles fp32 [frames])."""
-    g = generator
-    hf = (torch.rand(frames, device=device, generator=g) < 0.5).int()
-    vf = (torch.rand(frames, device=device, generator=g) < 0.5).int()
-    ang = (torch.rand(frames, device=device, generator=g) * 2.0 - 1.0) * degrees
-    return (hf | (vf << 1)).int(), ang.float()
+def pil_bilinear_coeffs(in_size, out_size):
+    """PIL's Image.resize(BILINEAR) coefficients along one axis (libImaging/Resample.c precompute_coeffs with the
+    triangle filter, support 1 scaled by max(1, in/out), then normalize_coeffs_8bpc's 22-bit fixed point):
+    (bounds int32 [out, 2] = (first source index, tap count), coeffs int32 [out, ksize], ksize)."""
+    scale = float(in_size) / out_size
+    filterscale = max(scale, 1.0)
+    support = 1.0 * filterscale
+    ksize = int(math.ceil(support)) * 2 + 1
+    bounds = np.zeros((out_size, 2), dtype=np.int32)
+    kk = np.zeros((out_size, ksize), dtype=np.int32)
+    ss = 1.0 / filterscale
+    for xx in range(out_size):
+        center = (xx + 0.5) * scale
+        xmin = max(int(center - support + 0.5), 0)          # C (int): truncation toward zero
+        xmax = min(int(center + support + 0.5), in_size) - xmin
+        w = []
+        ww = 0.0
+        for x in range(xmax):
+            t = abs((x + xmin - center + 0.5) * ss)
+            v = 1.0 - t if t < 1.0 else 0.0
+            w.append(v)
+            ww += v
+        for x in range(xmax):
+            k = w[x] / ww if ww != 0.0 else w[x]
+            kk[xx, x] = int(-0.5 + k * (1 << 22)) if k < 0 else int(0.5 + k * (1 << 22))
+        bounds[xx] = (xmin, xmax)
+    return bounds, kk, ksize
+
+
+def pil_rotate_fixed(angle, w, h):
+    """Image.rotate(angle, NEAREST, expand=False) of a w x h image as PIL 12 runs it: the inverse affine matrix
+    built in Image.rotate (angle % 360, cos / sin rounded to 15 decimals, rotation about (w/2, h/2)), then
+    libImaging affine_fixed's 16.16 fixed point with the pixel-centre offset folded into the translation.
+    Returns 8 int32 {on, a0, a1, a2, a3, a4, a5, 0}; on = 0 for the copy fast path (angle % 360 == 0).  The 180 /
+    90 / 270 transpose fast paths give the same map as this affine (exact rounded cos / sin)."""
+    angle = angle % 360.0
+    if angle == 0:
+        return [0] * 8
+    cx, cy = w / 2, h / 2
+    a = -math.radians(angle)
+    m = [round(math.cos(a), 15), round(math.sin(a), 15), 0.0, round(-math.sin(a), 15), round(math.cos(a), 15), 0.0]
+    m[2] = m[0] * -cx + m[1] * -cy + m[2] + cx
+    m[5] = m[3] * -cx + m[4] * -cy + m[5] + cy
+
+    def fix(v):
+        return math.floor(v * 65536.0 + 0.5)
+    return [1, fix(m[0]), fix(m[1]), fix(m[2] + m[1] * 0.5 + m[0] * 0.5), fix(m[3]), fix(m[4]),
+            fix(m[5] + m[4] * 0.5 + m[3] * 0.5), 0]
+
+
+@functools.lru_cache(maxsize=16)
+def _pil_axis(in_size, out_size):
+    b, k, ks = pil_bilinear_coeffs(in_size, out_size)
+    return b, k, ks
+
+
+def eval_size(H, W, short=224):
+    """torchvision T.Resize(int) output size (h, w): the shorter side to `short`, the longer scaled and truncated."""
+    if W <= H:
+        return int(short * H / W), short
+    return short, int(short * W / H)
+
+
+def draw_augment(frames, generator=None, degrees=90.0):
+    """Per-frame parameters of T.RandomHorizontalFlip, T.RandomVerticalFlip (p = 0.5) and T.RandomRotation(90),
+    drawn on the CPU in the order the reference's Compose draws them for each frame (torch.rand(1) < 0.5,
+    torch.rand(1) < 0.5, torch.empty(1).uniform_(-90, 90)): (flips int32 [frames] (bit 0 horizontal, bit 1
+    vertical), angles: list of Python floats)."""
+    flips, angles = [], []
+    for _ in range(frames):
+        hf = bool(torch.rand(1, generator=generator) < 0.5)
+        vf = bool(torch.rand(1, generator=generator) < 0.5)
+        ang = float(torch.empty(1).uniform_(-degrees, degrees, generator=generator).item())
+        flips.append(int(hf) | (int(vf) << 1))
+        angles.append(ang)
+    return torch.tensor(flips, dtype=torch.int32), angles
 
 
 def frame_augment(frames_u8, size=(224, 224), flips=None, angles=None, mean=IMAGENET_MEAN, std=IMAGENET_STD):
-    """uint8 [..., H, W, 3] decoded RGB frames -> fp32 [..., 3, size[1], size[0]]: Resize, flips, rotation,
-    ToTensor, Normalize (data_process.py:62-69).  flips / angles: per-frame device tensors (None: off)."""
-    *lead, H, W, c3 = frames_u8.shape
-    if c3 != 3 or frames_u8.dtype != torch.uint8:
-        raise ValueError("frame_augment expects uint8 [..., H, W, 3]")
-    x = frames_u8.contiguous()
-    n = x.numel() // (H * W * 3)
+    """uint8 [..., H, W, 3] decoded RGB frames (or [..., H, W] grey images) on the device -> fp32
+    [..., 3, size[1], size[0]]: PIL Resize, flips, rotation, ToTensor, Normalize (data_process.py:55-69 on PIL
+    images).  flips: int tensor [frames] (None: none); angles: per-frame rotation angles in degrees (host floats,
+    None: none)."""
+    x = frames_u8
+    if x.dtype != torch.uint8:
+        raise ValueError("frame_augment expects uint8 frames")
+    grey = x.shape[-1] != 3
+    *lead, H, W = (x.shape if grey else x.shape[:-1])
+    cin = 1 if grey else 3
+    x = x.contiguous()
+    n = x.numel() // (H * W * cin)
     ow, oh = size
-    out = torch.empty(*lead, 3, oh, ow, device=x.device, dtype=torch.float32)
-    fl = flips.to(torch.int32).contiguous() if flips is not None else None
-    an = angles.to(torch.float32).contiguous() if angles is not None else None
-    for t in (fl, an):
-        if t is not None and t.numel() != n:
-            raise ValueError("one flip / angle entry per frame")
-    L.check(L.lib().dfk_frame_augment(L.ptr(x), n, H, W, oh, ow, L.ptr(fl) if fl is not None else None,
-                                      L.ptr(an) if an is not None else None, _f3(mean), _f3(std), L.ptr(out),
-                                      L.stream()), "frame_augment")
+    dev = x.device
+    xb, xk, kx = _pil_axis(W, ow)
+    yb, yk, ky = _pil_axis(H, oh)
+    cxb, cxk = _const(("pilx", W, ow, "b"), lambda: xb, dev), _const(("pilx", W, ow, "k"), lambda: xk, dev)
+    cyb, cyk = _const(("pily", H, oh, "b"), lambda: yb, dev), _const(("pily", H, oh, "k"), lambda: yk, dev)
+    r = L.PilResize()
+    r.H, r.W, r.cin, r.out_h, r.out_w = H, W, cin, oh, ow
+    r.xb, r.xk, r.kx = cxb.data_ptr(), cxk.data_ptr(), kx
+    r.yb, r.yk, r.ky = cyb.data_ptr(), cyk.data_ptr(), ky
+    fl = flips.to(device=dev, dtype=torch.int32).contiguous() if flips is not None else None
+    aff = None
+    if angles is not None:
+        if len(angles) != n:
+            raise ValueError("one angle per frame")
+        aff = torch.tensor([pil_rotate_fixed(float(a), ow, oh) for a in angles], dtype=torch.int32).to(dev)
+    if fl is not None and fl.numel() != n:
+        raise ValueError("one flip entry per frame")
+    tmp = torch.empty(n * H * ow * cin, dtype=torch.uint8, device=dev)
+    out = torch.empty(*lead, 3, oh, ow, device=dev, dtype=torch.float32)
+    L.check(L.lib().dfk_frame_augment(L.ptr(x), n, r, L.ptr(fl) if fl is not None else None,
+                                      L.ptr(aff) if aff is not None else None, _f3(mean), _f3(std), L.ptr(tmp),
+                                      L.ptr(out), L.stream()), "frame_augment")
     return out

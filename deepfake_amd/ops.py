@@ -240,10 +240,13 @@ def _(wave, sr=22050, n_fft=2048, hop=512, n_mels=128, out_h=224, out_w=224):
 @torch.library.custom_op("dfk::frame_augment", mutates_args=())
 def frame_augment(frames: torch.Tensor, flips: torch.Tensor | None, angles: torch.Tensor | None, out_h: int = 224,
                   out_w: int = 224) -> torch.Tensor:
-    """The training frame transform (data_process.py:62-69) of uint8 [..., H, W, 3] frames."""
+    """The training frame transform (data_process.py:62-69, PIL semantics) of uint8 [..., H, W, 3] frames; angles
+    (degrees, one per frame) are read on the host (the rotation's fixed-point matrices are built there, as PIL
+    builds them)."""
     _need_gpu(frames)
     from . import media
-    return media.frame_augment(frames, (out_w, out_h), flips, angles)
+    ang = [float(a) for a in angles.detach().cpu().reshape(-1)] if angles is not None else None
+    return media.frame_augment(frames, (out_w, out_h), flips, ang)
 
 
 @frame_augment.register_fake

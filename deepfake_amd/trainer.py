@@ -58,33 +58,45 @@ def check_finite(loss, step):
     return loss
 
 
-def prepare_video(video, device, augment=False, generator=None):
+def prepare_video(video, device, augment=False, generator=None, size=224):
     """Frames to the device: fp32 transform output as is; decoded uint8 RGB frames [B,T,H,W,3] transformed on
-    the GPU -> [B,T,3,H,W]: T.ToTensor + T.Normalize (data/data_process.py:55-60, eval), or with augment the
-    training transform (:62-69: Resize, RandomHorizontalFlip, RandomVerticalFlip, RandomRotation(90), drawn per
-    frame as the reference transforms every frame separately)."""
+    the GPU -> [B,T,3,h,w] with the reference's torchvision transforms on PIL images (PIL semantics,
+    media.frame_augment): eval (data/data_process.py:55-60) T.Resize(224) (shorter side; a no-op on 224 x 224
+    frames, which then take the plain ToTensor + Normalize kernel) + ToTensor + Normalize; with augment the
+    training transform (:62-69: Resize((224, 224)), RandomHorizontalFlip, RandomVerticalFlip, RandomRotation(90),
+    drawn per frame in the reference's order, as it transforms every frame separately)."""
     from . import kernels as K
     from . import media
     v = video.to(device, non_blocking=True)
     if v.dtype != torch.uint8:
         return v
+    H, W = v.shape[-3], v.shape[-2]
     if not augment:
-        return K.frame_normalize(v)
-    n = v.numel() // (v.shape[-3] * v.shape[-2] * 3)
-    flips, angles = media.draw_augment(n, v.device, generator)
-    return media.frame_augment(v, flips=flips, angles=angles)
+        if min(H, W) == size:
+            return K.frame_normalize(v)
+        oh, ow = media.eval_size(H, W, size)
+        return media.frame_augment(v, (ow, oh))
+    n = v.numel() // (H * W * 3)
+    flips, angles = media.draw_augment(n, generator)
+    return media.frame_augment(v, (size, size), flips=flips, angles=angles)
 
 
-def prepare_mel(audio, device):
+def prepare_mel(audio, device, augment=False, generator=None, size=224):
     """The mel slot's input to the device: the normalised image as is; the uint8 grey image (the reference's
     cached JPEG, data_process.py:162) normalised on the GPU; a raw 22.05 kHz waveform [B, S] turned into the
-    mel-spectrogram image on the GPU first (generate_mel_spectrogram, src/utils.py:63-87)."""
+    mel-spectrogram image on the GPU first (generate_mel_spectrogram, src/utils.py:63-87).  augment: the
+    reference runs the mel JPEG through the same self.transform as the frames (data_process.py:162) — in training
+    Resize((224, 224)) + flips + RandomRotation(90), one draw per image (media.frame_augment on the grey image)."""
     from . import media
     a = audio.to(device, non_blocking=True)
+    if a.dtype != torch.uint8 and a.dim() == 2:
+        a = media.mel_image(a)
     if a.dtype == torch.uint8:
+        if augment:
+            n = a.numel() // (a.shape[-2] * a.shape[-1])
+            flips, angles = media.draw_augment(n, generator)
+            return media.frame_augment(a, (size, size), flips=flips, angles=angles)
         return media.gray_normalize(a)
-    if a.dim() == 2:
-        return media.gray_normalize(media.mel_image(a))
     return a
 
 
@@ -381,12 +393,12 @@ class Trainer:
         aug = self.augment and self.model.training
         if self.modality == "fused":
             wave = normalize_wave(pad_longest(feat["PAudio"]).to(self.device, non_blocking=True))
-            return (prepare_video(feat["Video"], self.device, aug), prepare_mel(feat["Audio"], self.device), wave)
+            return (prepare_video(feat["Video"], self.device, aug), prepare_mel(feat["Audio"], self.device, aug), wave)
         if self.modality == "paudio":
             return normalize_wave(pad_longest(feat).to(self.device, non_blocking=True))
         if self.modality == "video":
             return prepare_video(feat, self.device, aug)
-        return prepare_mel(feat, self.device)
+        return prepare_mel(feat, self.device, aug)
 
     def _prep(self, batch):
         return self._features(batch[0]), batch[1].to(self.device, non_blocking=True)

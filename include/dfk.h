@@ -377,13 +377,28 @@ int dfk_mel_image(const float* wave, int64_t B, int64_t S, const float* basis, c
  * (data_process.py:55-69,162); mean3 / std3 are HOST arrays of 3 floats. */
 int dfk_gray_normalize(const uint8_t* src, float* dst, int64_t n_img, int32_t H, int32_t W, const float* mean3,
                        const float* std3, hipStream_t stream);
-/* Train-time frame transform of data_process.py:62-69 fused per output pixel: T.Resize((out_h, out_w)) (bilinear,
- * half-pixel centres, rounded to uint8), T.RandomHorizontalFlip (flips[f] bit 0), T.RandomVerticalFlip (bit 1),
- * T.RandomRotation (angles[f] degrees; torchvision F.rotate on tensors: nearest, fill 0, no expand),
- * T.ToTensor + T.Normalize.  src uint8 [frames, H, W, 3] (decoded RGB), dst fp32 [frames, 3, out_h, out_w];
- * flips / angles are DEVICE arrays of one entry per frame (NULL: no flip / no rotation); mean3 / std3 HOST. */
-int dfk_frame_augment(const uint8_t* src, int64_t frames, int32_t H, int32_t W, int32_t out_h, int32_t out_w,
-                      const int32_t* flips, const float* angles, const float* mean3, const float* std3, float* dst,
+/* Frame transform of data_process.py:55-69 as the reference runs it — torchvision transforms on PIL images
+ * (src/utils.py:32-33 Image.fromarray; the mel JPEG at :162 through the same transform):
+ *   T.Resize -> PIL Image.resize(BILINEAR): separable, width pass then height pass, each into uint8 — a triangle
+ *     filter whose support scales with the downscale factor (antialiased), per-output-pixel coefficients in PIL's
+ *     22-bit fixed point (bounds [out][2] = first source index, tap count; coefficients [out][k]), built on the host
+ *     by deepfake_amd.media.pil_bilinear_coeffs exactly as PIL's precompute_coeffs / normalize_coeffs_8bpc;
+ *   T.RandomHorizontalFlip (flips[f] bit 0), T.RandomVerticalFlip (bit 1): Image.transpose;
+ *   T.RandomRotation -> Image.rotate(angle, NEAREST, fill 0): affine[f] = 8 int32 {on, a0, a1, a2, a3, a4, a5, 0},
+ *     PIL affine_fixed's 16.16 inverse map (source x = (a2 + x a0 + y a1) >> 16, y = (a5 + x a3 + y a4) >> 16) of
+ *     the matrix PIL builds (media.pil_rotate_fixed); on = 0: no rotation;
+ *   T.ToTensor + T.Normalize.
+ * src uint8 [frames][H][W][cin] (cin 3: decoded RGB; cin 1: a grey image converted to RGB); tmp uint8 scratch of
+ * frames*H*out_w*cin bytes (the width pass); dst fp32 [frames][3][out_h][out_w].  flips / affine: DEVICE arrays
+ * (NULL: none); mean3 / std3: HOST arrays of 3 floats. */
+typedef struct {
+  int32_t H, W, cin;
+  int32_t out_h, out_w;
+  const int32_t* xb; const int32_t* xk; int32_t kx;
+  const int32_t* yb; const int32_t* yk; int32_t ky;
+} dfk_pil_resize;
+int dfk_frame_augment(const uint8_t* src, int64_t frames, const dfk_pil_resize* rs, const int32_t* flips,
+                      const int32_t* affine, const float* mean3, const float* std3, uint8_t* tmp, float* dst,
                       hipStream_t stream);
 
 /* ---- 2-D convolution family of the Inception-ResNet-v2 video branch (SURVEY.md §8f f4:

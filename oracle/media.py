@@ -9,10 +9,14 @@ PIL/torchvision), so it is restated from their published algorithms:
       top_db=80);
   OpenCV 4: normalize(NORM_MINMAX, 0, 255) (double scale / shift), astype(uint8) truncation,
       resize(INTER_LINEAR) on uint8 (11-bit fixed-point coefficients, 22-bit rounding shift);
-  torchvision (tensor path): F.rotate (inverse affine grid of pixel centres, grid_sample nearest,
-      fill 0), hflip / vflip, ToTensor, Normalize.
-No golden vectors exist for these (the reference has no tests and the libraries are absent):
-PARITY UNPINNED against librosa / cv2 / PIL; the STFT stage is checked against torch.stft.
+  PIL 12.2 (the frame / mel-image transform: torchvision's transforms run on PIL images in the reference,
+      src/utils.py:32-33, data_process.py:55-69,162): Image.resize(BILINEAR) (libImaging/Resample.c: triangle
+      filter with support scaled by the downscale factor, 22-bit fixed-point coefficients, width pass then height
+      pass, each into uint8), Image.rotate(NEAREST, fill 0) (Image.rotate's inverse matrix, affine_fixed's 16.16
+      fixed-point walk), transpose flips.
+The PIL restatement is pinned bit for bit to fixtures written with PIL itself (tests/golden/pil_frames.npz,
+tests/golden/make_pil_fixtures.py).  librosa / cv2 are absent: the mel-spectrogram stage is PARITY UNPINNED
+against them; its STFT is checked against torch.stft.
 """
 import math
 
@@ -110,3 +114,76 @@ def cv_resize_linear_u8(img, size):
 def mel_image(y, sr=22050, n_fft=2048, hop=512, n_mels=128, size=(224, 224)):
     """generate_mel_spectrogram from the decoded waveform on (the file I/O and the resampling excluded)."""
     return cv_resize_linear_u8(mel_db_uint8(y, sr, n_fft, hop, n_mels), size)
+
+
+# ---------------------------------------------------------------- PIL 12.2 frame transform
+def pil_coeffs(in_size, out_size):
+    """libImaging/Resample.c precompute_coeffs (BILINEAR: triangle, support 1) + normalize_coeffs_8bpc."""
+    scale = float(in_size) / out_size
+    fscale = max(scale, 1.0)
+    support = fscale
+    taps = []
+    for xx in range(out_size):
+        center = (xx + 0.5) * scale
+        xmin = max(int(center - support + 0.5), 0)
+        xmax = min(int(center + support + 0.5), in_size) - xmin
+        w = [max(0.0, 1.0 - abs((x + xmin - center + 0.5) / fscale)) for x in range(xmax)]
+        ww = 0.0
+        for v in w:
+            ww += v
+        k = [(v / ww if ww != 0.0 else v) for v in w]
+        taps.append((xmin, [int(-0.5 + v * (1 << 22)) if v < 0 else int(0.5 + v * (1 << 22)) for v in k]))
+    return taps
+
+
+def _pass(img, taps, axis):
+    """One separable pass over `axis` of a uint8 [h, w, c] image (22-bit rounding, clip to uint8)."""
+    im = np.moveaxis(img.astype(np.int64), axis, 0)
+    out = np.empty((len(taps),) + im.shape[1:], dtype=np.uint8)
+    for o, (x0, k) in enumerate(taps):
+        acc = np.full(im.shape[1:], 1 << 21, dtype=np.int64)
+        for t, kv in enumerate(k):
+            acc += im[x0 + t] * kv
+        out[o] = np.clip(acc >> 22, 0, 255)
+    return np.moveaxis(out, 0, axis)
+
+
+def pil_resize_bilinear(img, size):
+    """Image.resize((w, h), BILINEAR) of a uint8 [h, w, c] image: width pass, then height pass."""
+    ow, oh = size
+    h, w = img.shape[:2]
+    return _pass(_pass(img, pil_coeffs(w, ow), 1), pil_coeffs(h, oh), 0)
+
+
+def pil_rotate_nearest(img, angle):
+    """Image.rotate(angle, NEAREST, expand=False, fillcolor=0) of a uint8 [h, w, c] image."""
+    angle = angle % 360.0
+    if angle == 0:
+        return img.copy()
+    h, w = img.shape[:2]
+    cx, cy = w / 2, h / 2
+    a = -math.radians(angle)
+    m = [round(math.cos(a), 15), round(math.sin(a), 15), 0.0, round(-math.sin(a), 15), round(math.cos(a), 15), 0.0]
+    m[2] = m[0] * -cx + m[1] * -cy + m[2] + cx
+    m[5] = m[3] * -cx + m[4] * -cy + m[5] + cy
+    fix = lambda v: math.floor(v * 65536.0 + 0.5)  # noqa: E731
+    a0, a1, a3, a4 = fix(m[0]), fix(m[1]), fix(m[3]), fix(m[4])
+    a2, a5 = fix(m[2] + m[1] * 0.5 + m[0] * 0.5), fix(m[5] + m[4] * 0.5 + m[3] * 0.5)
+    y, x = np.mgrid[0:h, 0:w].astype(np.int64)
+    xin = (a2 + x * a0 + y * a1) >> 16
+    yin = (a5 + x * a3 + y * a4) >> 16
+    ok = (xin >= 0) & (xin < w) & (yin >= 0) & (yin < h)
+    out = np.zeros_like(img)
+    out[ok] = img[yin[ok], xin[ok]]
+    return out
+
+
+def pil_train_transform(img, flip, angle, size=224):
+    """Resize((size, size)) -> RandomHorizontalFlip (flip bit 0) -> RandomVerticalFlip (bit 1) -> RandomRotation
+    (angle) on a uint8 [h, w, 3] image, as uint8 (data_process.py:62-69 before ToTensor / Normalize)."""
+    r = pil_resize_bilinear(img, (size, size))
+    if flip & 1:
+        r = r[:, ::-1]
+    if flip & 2:
+        r = r[::-1]
+    return pil_rotate_nearest(np.ascontiguousarray(r), angle)

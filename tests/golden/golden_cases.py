@@ -112,3 +112,22 @@ def fixture_compress(key, a, big=65536, sample=8192):
     return {key + "@sub": a.reshape(-1)[::step].copy(), key + "@step": np.array(step),
             key + "@shape": np.array(a.shape), key + "@sum": np.array(f.sum()),
             key + "@norm": np.array(np.sqrt((f * f).sum()))}
+
+
+# ---------------------------------------------------------------- f2: PIL frame transform fixtures
+PIL_FRAMES = dict(name="pil_frames", seed=201)
+
+
+def pil_test_image(seed, h, w, channels=3):
+    """Deterministic decoded-frame stand-in (uint8 [h, w, channels]): smooth gradients and blobs with noise, so
+    the antialiased resize sees real structure at every scale (regenerated by the tests, never stored)."""
+    import numpy as np
+    g = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+    out = np.empty((h, w, channels), dtype=np.uint8)
+    for c in range(channels):
+        fx, fy, ph = g.uniform(2, 40), g.uniform(2, 40), g.uniform(0, 6.28)
+        v = 128 + 60 * np.sin(2 * np.pi * x / w * fx + ph) * np.cos(2 * np.pi * y / h * fy) + 40 * (x / w - y / h)
+        v += g.normal(0, 12, size=(h, w))
+        out[..., c] = np.clip(np.rint(v), 0, 255).astype(np.uint8)
+    return out[..., 0] if channels == 1 else out

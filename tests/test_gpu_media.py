@@ -2,10 +2,10 @@
 Mel image: the reference's generate_mel_spectrogram pipeline (src/utils.py:63-87) restated in numpy —
 PARITY UNPINNED against librosa / cv2 (absent from the image); bars: at most 1 grey level apart, >= 99.5 %
 of pixels identical (fp32 MFMA STFT vs float64 FFT: only values within ~1e-4 of a quantisation boundary flip).
-Frame transform (data_process.py:62-69): flips bit-exact vs torch.flip, rotation vs torchvision's tensor
-F.rotate restated with torch.nn.functional.grid_sample (nearest; >= 99.9 % identical, ties of the nearest
-rounding may differ in the last fp32 ulp), resize vs torch F.interpolate(bilinear) rounded to uint8."""
-import math
+Frame / mel-image transform (data_process.py:55-69,162 — torchvision transforms on PIL images): bit-exact
+against fixtures written by PIL 12.2 itself (tests/golden/pil_frames.npz: antialiased BILINEAR resize from
+1280x720 / 320x180 / 150x100 frames, flips, NEAREST rotation, the eval shorter-side resize, the grey mel image),
+then ToTensor + Normalize in fp32."""
 
 import numpy as np
 import pytest
@@ -27,7 +27,7 @@ def _norm(u8_chw):
     return x.float().div(255).sub(MEAN.view(3, 1, 1)).div(STD.view(3, 1, 1))
 
 
-@pytest.mark.parametrize("seconds", [1, 4])
+@pytest.mark.parametrize("seconds", [1, 4, 14])   # 14 s: a 603-frame image, > 64 KB of LDS
 def test_mel_image_matches_oracle(seconds):
     from deepfake_amd import media
     g = np.random.default_rng(seconds)
@@ -57,29 +57,46 @@ def test_gray_normalize_exact():
     assert torch.equal(out, ref)
 
 
-def _rotate_ref(img_chw, angle):
-    """torchvision.transforms.functional.rotate (tensor path, nearest, fill 0, expand False) restated."""
-    C, h, w = img_chw.shape
-    rot = math.radians(-angle)
-    theta = torch.tensor([[math.cos(rot), math.sin(rot), 0.0], [-math.sin(rot), math.cos(rot), 0.0]],
-                         dtype=torch.float32).view(1, 2, 3)
-    base = torch.empty(1, h, w, 3)
-    base[..., 0].copy_(torch.linspace(-w * 0.5 + 0.5, w * 0.5 + 0.5 - 1, steps=w))
-    base[..., 1].copy_(torch.linspace(-h * 0.5 + 0.5, h * 0.5 + 0.5 - 1, steps=h).unsqueeze(-1))
-    base[..., 2].fill_(1)
-    grid = base.view(1, h * w, 3).bmm(theta.transpose(1, 2) / torch.tensor([0.5 * w, 0.5 * h])).view(1, h, w, 2)
-    return F.grid_sample(img_chw.unsqueeze(0).float(), grid, mode="nearest", padding_mode="zeros",
-                         align_corners=False)[0]
+def _pil_fixture():
+    import golden_cases as GC
+    from fixtures import load
+    return GC, load(GC.PIL_FRAMES["name"])
 
 
-def test_frame_augment_flips_rotation_resize():
+@pytest.mark.parametrize("name,h,w,ch", [("resize720", 720, 1280, 3), ("aug180", 180, 320, 3), ("aug720", 720, 1280, 3),
+                                         ("mel224", 224, 224, 1), ("aug_up", 100, 150, 3)])
+def test_frame_augment_matches_pil(name, h, w, ch):
+    """dfk_frame_augment (PIL resize + flips + rotation + ToTensor + Normalize) against PIL's own output,
+    bit for bit; grey images (the mel JPEG) take the 1-channel path."""
+    from deepfake_amd import media
+    GC, fx = _pil_fixture()
+    base, n = int(fx[name + ":seed"]), fx[name].shape[0]
+    src = torch.from_numpy(np.stack([GC.pil_test_image(base + i, h, w, ch) for i in range(n)])).to(DEV)
+    aug = name != "resize720"
+    flips = torch.from_numpy(fx[name + ":flips"]) if aug else None
+    angles = [float(a) for a in fx[name + ":angles"]] if aug else None
+    out = media.frame_augment(src, flips=flips, angles=angles).cpu()
+    ref = torch.stack([_norm(torch.from_numpy(fx[name][i]).permute(2, 0, 1)) for i in range(n)])
+    assert torch.equal(out, ref), int((out != ref).any(1).sum())
+
+
+def test_frame_eval_resize_matches_pil():
+    """Eval T.Resize(224) of a 1280x720 frame (shorter side to 224 -> 224 x 398) via prepare_video."""
+    from deepfake_amd.trainer import prepare_video
+    GC, fx = _pil_fixture()
+    src = torch.from_numpy(GC.pil_test_image(GC.PIL_FRAMES["seed"] * 1000 + 999, 720, 1280, 3))[None, None]
+    out = prepare_video(src, DEV, augment=False).cpu()
+    assert out.shape == (1, 1, 3, 224, 398)
+    assert torch.equal(out[0, 0], _norm(torch.from_numpy(fx["eval720"][0]).permute(2, 0, 1)))
+
+
+def test_frame_augment_identity_and_flips():
     from deepfake_amd import media
     from deepfake_amd import kernels as K
-    n, H, W = 6, 224, 224
-    fr = torch.randint(0, 256, (n, H, W, 3), dtype=torch.uint8, device=DEV)
-    # identity transform == ToTensor + Normalize (dfk_frame_normalize), bit for bit
-    assert torch.equal(media.frame_augment(fr), K.frame_normalize(fr))
-    flips = torch.tensor([0, 1, 2, 3, 1, 2], dtype=torch.int32, device=DEV)
+    n = 4
+    fr = torch.randint(0, 256, (n, 224, 224, 3), dtype=torch.uint8, device=DEV)
+    assert torch.equal(media.frame_augment(fr), K.frame_normalize(fr))   # 224 -> 224: PIL's copy
+    flips = torch.tensor([0, 1, 2, 3], dtype=torch.int32)
     out = media.frame_augment(fr, flips=flips).cpu()
     for i in range(n):
         x = fr[i].permute(2, 0, 1)
@@ -88,24 +105,6 @@ def test_frame_augment_flips_rotation_resize():
         if flips[i] & 2:
             x = torch.flip(x, [1])
         assert torch.equal(out[i], _norm(x)), i
-    angles = torch.tensor([0.0, 37.5, -90.0, 90.0, 12.25, -61.0], device=DEV)
-    out = media.frame_augment(fr, flips=flips, angles=angles).cpu()
-    for i in range(n):
-        x = fr[i].permute(2, 0, 1).cpu()
-        if flips[i] & 1:
-            x = torch.flip(x, [2])
-        if flips[i] & 2:
-            x = torch.flip(x, [1])
-        ref = _norm(_rotate_ref(x, float(angles[i])).round().to(torch.uint8))
-        same = (out[i] == ref).all(0).float().mean().item()
-        assert same >= 0.999, (i, same)
-    # resize from a decoded 180x320 frame: torch bilinear (half-pixel centres) rounded to uint8
-    src = torch.randint(0, 256, (2, 180, 320, 3), dtype=torch.uint8, device=DEV)
-    out = media.frame_augment(src).cpu()
-    ref = F.interpolate(src.permute(0, 3, 1, 2).float().cpu(), size=(224, 224), mode="bilinear", align_corners=False)
-    ref = torch.stack([_norm(r.round().clamp(0, 255).to(torch.uint8)) for r in ref])
-    same = (out == ref).all(1).float().mean().item()
-    assert same >= 0.999, same
 
 
 def test_trainer_media_inputs():
@@ -119,8 +118,16 @@ def test_trainer_media_inputs():
     frames = torch.randint(0, 256, (2, 4, 112, 112, 3), generator=g, dtype=torch.uint8)
     v = prepare_video(frames, DEV, augment=True)
     assert v.shape == (2, 4, 3, 224, 224) and torch.isfinite(v).all()
-    v0 = prepare_video(frames, DEV, augment=False)
-    assert torch.equal(v0, K.frame_normalize(frames.to(DEV)))
+    f224 = torch.randint(0, 256, (2, 4, 224, 224, 3), generator=g, dtype=torch.uint8)
+    assert torch.equal(prepare_video(f224, DEV, augment=False), K.frame_normalize(f224.to(DEV)))
+    # the mel slot under --augment: the grey image through the frames' training transform (data_process.py:162),
+    # the same draws as the frame path's for the same generator state
+    gray0 = torch.randint(0, 256, (2, 224, 224), generator=g, dtype=torch.uint8)
+    ga, gb = torch.Generator().manual_seed(5), torch.Generator().manual_seed(5)
+    ma = prepare_mel(gray0, DEV, augment=True, generator=ga)
+    flips, angles = media.draw_augment(2, gb)
+    assert torch.equal(ma, media.frame_augment(gray0.to(DEV), flips=flips, angles=angles))
+    assert not torch.equal(ma, media.gray_normalize(gray0.to(DEV)))
     wave = 0.1 * torch.randn(2, 22050 * 2, generator=g)
     m = prepare_mel(wave, DEV)
     assert m.shape == (2, 3, 224, 224) and torch.isfinite(m).all()

@@ -53,3 +53,46 @@ def test_product_constants_match_oracle():
     got = fr @ b
     assert np.abs(got[:1025] - X.real).max() < 1e-4 and np.abs(got[1025:2050] - X.imag).max() < 1e-4
     assert b.shape == (2048, 2052) and not b[:, 2050:].any()
+
+
+def _pil_cases():
+    import golden_cases as GC
+    from fixtures import load
+    fx = load(GC.PIL_FRAMES["name"])
+    shapes = {"resize720": (720, 1280, 3), "aug180": (180, 320, 3), "aug720": (720, 1280, 3), "mel224": (224, 224, 1),
+              "aug_up": (100, 150, 3)}
+    return GC, fx, shapes
+
+
+def test_pil_restatement_matches_pil_fixtures():
+    """oracle/media.py's PIL 12.2 restatement (antialiased BILINEAR resize, NEAREST rotation, flips) equals the
+    fixtures PIL itself wrote (tests/golden/make_pil_fixtures.py), bit for bit."""
+    GC, fx, shapes = _pil_cases()
+    for name, (h, w, ch) in shapes.items():
+        base = int(fx[name + ":seed"])
+        for i in range(fx[name].shape[0]):
+            img = GC.pil_test_image(base + i, h, w, ch)
+            if ch == 1:
+                img = np.repeat(img[..., None], 3, axis=2)
+            if name == "resize720":
+                got = OM.pil_resize_bilinear(img, (224, 224))
+            else:
+                got = OM.pil_train_transform(img, int(fx[name + ":flips"][i]), float(fx[name + ":angles"][i]))
+            assert np.array_equal(got, fx[name][i]), (name, i, int((got != fx[name][i]).sum()))
+    img = GC.pil_test_image(GC.PIL_FRAMES["seed"] * 1000 + 999, 720, 1280, 3)
+    assert np.array_equal(OM.pil_resize_bilinear(img, (398, 224)), fx["eval720"][0])
+
+
+def test_product_pil_constants_match_oracle():
+    """The host-built constants the kernel reads (deepfake_amd.media: resize coefficients, rotation matrices)
+    equal the oracle's restatement."""
+    import math
+    from deepfake_amd import media
+    for n_in, n_out in ((1280, 224), (720, 224), (180, 224), (224, 224), (150, 224), (1280, 398)):
+        b, k, ks = media.pil_bilinear_coeffs(n_in, n_out)
+        taps = OM.pil_coeffs(n_in, n_out)
+        for o, (x0, kv) in enumerate(taps):
+            assert b[o, 0] == x0 and b[o, 1] == len(kv) and list(k[o, :len(kv)]) == kv and not k[o, len(kv):].any()
+    for ang in (0.0, 37.5, -61.25, 90.0, 180.0, -89.99):
+        m = media.pil_rotate_fixed(ang, 224, 224)
+        assert (m[0] == 0) == (ang % 360.0 == 0)
