@@ -18,19 +18,27 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // This file is built with IEEE mode off and no-NaN semantics (build.py FILE_FLAGS).  The device library's ockl
-// functions behind threadIdx / blockIdx / blockDim / gridDim / __umulhi carry the default attributes, so hipcc does
-// not inline them here: each use compiled to an s_swappc call (346 in this object, inside the K / V / Q gather
-// loops of every attention kernel).  These builtins are the inline instructions / dispatch-packet reads instead.
+// functions behind threadIdx / blockIdx / __umulhi carry the default attributes, so hipcc does not inline them
+// here: each use compiled to an s_swappc call (346 in this object, inside the K / V / Q gather loops of every
+// attention kernel).  The work-item / work-group ids and the multiply-high below are inline instructions.
+#ifdef DFK_OCKL_ALL
+__device__ __forceinline__ int dfk_tid() { return threadIdx.x; }
+__device__ __forceinline__ int dfk_bid_x() { return blockIdx.x; }
+__device__ __forceinline__ int dfk_bid_y() { return blockIdx.y; }
+__device__ __forceinline__ int dfk_bid_z() { return blockIdx.z; }
+__device__ __forceinline__ uint32_t dfk_umulhi(uint32_t a, uint32_t b) { return __umulhi(a, b); }
+#else
 __device__ __forceinline__ int dfk_tid() { return (int)__builtin_amdgcn_workitem_id_x(); }
 __device__ __forceinline__ int dfk_bid_x() { return (int)__builtin_amdgcn_workgroup_id_x(); }
 __device__ __forceinline__ int dfk_bid_y() { return (int)__builtin_amdgcn_workgroup_id_y(); }
 __device__ __forceinline__ int dfk_bid_z() { return (int)__builtin_amdgcn_workgroup_id_z(); }
-__device__ __forceinline__ int dfk_bdim() { return (int)__builtin_amdgcn_workgroup_size_x(); }
-__device__ __forceinline__ int dfk_gdim_x() {
-  const unsigned w = __builtin_amdgcn_workgroup_size_x();
-  return (int)((__builtin_amdgcn_grid_size_x() + w - 1) / w);
-}
 __device__ __forceinline__ uint32_t dfk_umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+#endif
+// blockDim / gridDim stay HIP's: the dispatch-packet builtins (__builtin_amdgcn_workgroup_size_x / grid_size_x)
+// measured slower in every attention kernel (mel1 forward 13.8 -> 36.5 us, vst3 52.9 -> 76.3 us: r4 A/B,
+// profiles/attn/r4h_builtin_dims_ab.txt)
+__device__ __forceinline__ int dfk_bdim() { return blockDim.x; }
+__device__ __forceinline__ int dfk_gdim_x() { return gridDim.x; }
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 struct TokInfo {

@@ -299,6 +299,69 @@ class SwinTransformer3D(nn.Module):
                 for p in self.layers[i].parameters():
                     p.requires_grad = False
 
+    @staticmethod
+    def _init_module(m):
+        """video_swin_transformer.py:578-585 / :643-650: Linear weights trunc_normal(std .02), biases 0; LayerNorm 1 / 0."""
+        if isinstance(m, nn.Linear):
+            nn.init.trunc_normal_(m.weight, std=.02)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+
+    def inflate_weights(self, logger=print):
+        """video_swin_transformer.py:566-632: load a 2-D Swin checkpoint ({'model': state_dict}) into this 3-D model —
+        relative_position_index / attn_mask entries dropped (re-initialised here), patch_embed.proj.weight repeated
+        over the patch depth and divided by it, relative_position_bias_table bicubic-resized to (2Wh-1, 2Ww-1) when
+        its side differs and repeated 2Wd-1 times; strict=False.  Loaded with weights_only=True (tensors only)."""
+        self.apply(self._init_module)
+        checkpoint = torch.load(self.pretrained, map_location="cpu", weights_only=True)
+        state_dict = dict(checkpoint["model"])
+        for k in [k for k in state_dict if "relative_position_index" in k or "attn_mask" in k]:
+            del state_dict[k]
+        pd = self.patch_size[0]
+        state_dict["patch_embed.proj.weight"] = state_dict["patch_embed.proj.weight"].unsqueeze(2).repeat(1, 1, pd, 1, 1) / pd
+        own = self.state_dict()
+        wd, wh, ww = self.window_size
+        for k in [k for k in state_dict if "relative_position_bias_table" in k]:
+            t = state_dict[k]
+            L1, nH1 = t.size()
+            nH2 = own[k].size(1)
+            L2 = (2 * wh - 1) * (2 * ww - 1)
+            if nH1 != nH2:
+                logger(f"Error in loading {k}, passing")
+            elif L1 != L2:
+                S1 = int(L1 ** 0.5)
+                t = torch.nn.functional.interpolate(t.permute(1, 0).view(1, nH1, S1, S1), size=(2 * wh - 1, 2 * ww - 1),
+                                                    mode="bicubic").view(nH2, L2).permute(1, 0)
+            state_dict[k] = t.repeat(2 * wd - 1, 1)
+        msg = self.load_state_dict(state_dict, strict=False)
+        logger(msg)
+        logger(f"=> loaded successfully '{self.pretrained}'")
+
+    def init_weights(self, pretrained=None):
+        """video_swin_transformer.py:634-666: re-initialise (Linear trunc_normal, LayerNorm 1 / 0), then inflate a 2-D
+        checkpoint (pretrained2d) or load a 3-D one ({'state_dict' | plain} state_dict, 'module.' / 'backbone.'
+        prefixes stripped, strict=False: mmcv load_checkpoint's behaviour for this backbone)."""
+        if pretrained:
+            self.pretrained = pretrained
+        if isinstance(self.pretrained, str):
+            self.apply(self._init_module)
+            if self.pretrained2d:
+                self.inflate_weights()
+            else:
+                ck = torch.load(self.pretrained, map_location="cpu", weights_only=True)
+                sd = ck.get("state_dict", ck) if isinstance(ck, dict) else ck
+                sd = {(k[7:] if k.startswith("module.") else k): v for k, v in sd.items()}
+                if any(k.startswith("backbone.") for k in sd):
+                    sd = {k[9:]: v for k, v in sd.items() if k.startswith("backbone.")}
+                self.load_state_dict(sd, strict=False)
+        elif self.pretrained is None:
+            self.apply(self._init_module)
+        else:
+            raise TypeError("pretrained must be a str or None")
+
     def forward_tokens(self, x, layout="bcthw"):
         """-> final-LN channels-last [B, D', H', W', 8C] in the compute dtype."""
         x = self.patch_embed.tokens(x, layout)

@@ -77,3 +77,58 @@ def seed_torch(seed):
     os.environ["PYTHONHASHSEED"] = str(seed)
     np.random.seed(seed)
     torch.manual_seed(seed)
+
+
+def _strip_module(sd, skip=None):
+    """src/utils.py:269-289: drop the first 7 characters ('module.' of a DataParallel checkpoint) of every key."""
+    return {k[7:]: v for k, v in sd.items() if not (skip and skip in k)}
+
+
+def load_pre_fused(args, VE, AE, PAE, logger=print):
+    """src/utils.py:262-292: fine-tuned single-modality checkpoints ({'checkpoint': state_dict} of a DataParallel
+    model) into the fused model's extractors — audio (SwinV2) without its 'head' keys, strict=False; video and
+    paudio strict.  torch.load(weights_only=True): tensors only."""
+    for path, mod, skip, strict, what in ((getattr(args, "audio_ckpt_path", None), AE, "head", False, "Audio"),
+                                          (getattr(args, "video_ckpt_path", None), VE, None, True, "Video"),
+                                          (getattr(args, "paudio_ckpt_path", None), PAE, None, True, "PAudio")):
+        if path is None:
+            continue
+        logger(f"==============> Loading weight {path} for {what} fine-tuning......")
+        ck = torch.load(path, map_location="cpu", weights_only=True)["checkpoint"]
+        mod.load_state_dict(_strip_module(ck, skip), strict=strict)
+        logger(f"=> loaded successfully '{path}'")
+
+
+def load_pretrained(config, model, logger=print):
+    """src/utils.py:294-380 (the SwinV2 audio branch): {'checkpoint': state_dict} with relative_position_index /
+    relative_coords_table / attn_mask dropped (re-initialised here), relative_position_bias_table and
+    absolute_pos_embed bicubic-resized when their size differs, strict=False."""
+    import torch.nn.functional as F
+    path = config.audio_ckpt_path
+    logger(f"==============> Loading weight {path} for fine-tuning......")
+    state_dict = dict(torch.load(path, map_location="cpu", weights_only=True)["checkpoint"])
+    for k in [k for k in state_dict if "relative_position_index" in k or "relative_coords_table" in k or
+              "attn_mask" in k]:
+        del state_dict[k]
+    own = model.state_dict()
+    for k in [k for k in state_dict if "relative_position_bias_table" in k]:
+        t = state_dict[k]
+        L1, nH1 = t.size()
+        L2, nH2 = own[k].size()
+        if nH1 != nH2:
+            logger(f"Error in loading {k}, passing......")
+        elif L1 != L2:
+            S1, S2 = int(L1 ** 0.5), int(L2 ** 0.5)
+            state_dict[k] = F.interpolate(t.permute(1, 0).view(1, nH1, S1, S1), size=(S2, S2),
+                                          mode="bicubic").view(nH2, L2).permute(1, 0)
+    for k in [k for k in state_dict if "absolute_pos_embed" in k]:
+        t = state_dict[k]
+        _, L1, C1 = t.size()
+        _, L2, _ = own[k].size()
+        if L1 != L2:
+            S1, S2 = int(L1 ** 0.5), int(L2 ** 0.5)
+            t = F.interpolate(t.reshape(-1, S1, S1, C1).permute(0, 3, 1, 2), size=(S2, S2), mode="bicubic")
+            state_dict[k] = t.permute(0, 2, 3, 1).flatten(1, 2)
+    msg = model.load_state_dict(state_dict, strict=False)
+    logger(msg)
+    logger(f"=> loaded successfully '{getattr(config, 'audio_pretrained_dir', path)}'")

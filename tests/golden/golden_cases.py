@@ -131,3 +131,50 @@ def pil_test_image(seed, h, w, channels=3):
         v += g.normal(0, 12, size=(h, w))
         out[..., c] = np.clip(np.rint(v), 0, 255).astype(np.uint8)
     return out[..., 0] if channels == 1 else out
+
+
+# ---------------------------------------------------------------- pretrained-weight loaders
+PRETRAINED = dict(name="pretrained", seed=211,
+                  vst=dict(patch_size=(2, 4, 4), embed_dim=96, depths=[2, 2, 2, 2], num_heads=[3, 6, 12, 24],
+                           window_size=(4, 7, 7), patch_norm=True),
+                  mel=dict(num_classes=1, use_feat=True, img_size=224, embed_dim=32, depths=[2, 2, 2, 2],
+                           num_heads=[1, 2, 4, 8], window_size=7, pretrained_window_sizes=(16, 16, 16, 16)))
+
+
+def synth_swin2d_checkpoint(shapes, seed):
+    """A 2-D Swin checkpoint {'model': state_dict} for a 3-D model with the given {key: shape}: every key with the
+    2-D shape — patch_embed.proj.weight without the patch-depth axis, relative_position_bias_table [(2*12-1)^2, nH]
+    (a window-12 pretraining: bicubic-resized on load) in stages 0-1 and [(2*7-1)^2, nH] in stages 2-3 — plus
+    entries the loader must drop (relative_position_index, attn_mask) and one it must ignore (head.weight)."""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for k, shp in shapes.items():
+        if k == "patch_embed.proj.weight":
+            shp = (shp[0], shp[1], shp[3], shp[4])
+        elif "relative_position_bias_table" in k:
+            side = 23 if k.startswith(("layers.0.", "layers.1.")) else 13
+            shp = (side * side, shp[1])
+        elif "relative_position_index" in k:
+            sd[k] = torch.zeros(169, 169, dtype=torch.long)
+            continue
+        sd[k] = torch.randn(shp, generator=g) * 0.02
+    sd["layers.0.blocks.1.attn_mask"] = torch.full((4, 49, 49), -100.0)
+    sd["head.weight"] = torch.randn(10, 768, generator=g)
+    return {"model": sd}
+
+
+def synth_swinv2_checkpoint(shapes, seed):
+    """{'checkpoint': state_dict} for a SwinV2 model: every parameter random, and the re-initialised buffers
+    (relative_coords_table, relative_position_index) filled with garbage the loader must drop."""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for k, shp in shapes.items():
+        if "relative_position_index" in k:
+            sd[k] = torch.zeros(shp, dtype=torch.long)
+        elif "relative_coords_table" in k:
+            sd[k] = torch.full(shp, 7.0)
+        else:
+            sd[k] = torch.randn(shp, generator=g) * 0.05
+    return {"checkpoint": sd}

@@ -100,6 +100,37 @@ def case_block_c4():
     _block(GC.BLOCK_C4_S3)
 
 
+def case_pretrained():
+    """The reference's pretrained-weight loaders on synthetic checkpoints: SwinTransformer3D.inflate_weights
+    (video_swin_transformer.py:566-632: 2-D -> 3-D patch-embed repeat / depth, bicubic RPB resize, repeat 2Wd-1) and
+    the SwinV2 load_pretrained (src/utils.py:294-380).  Stores the loaded tensors (the randomly re-initialised rest
+    is not comparable)."""
+    import tempfile
+    c = GC.PRETRAINED
+    m = VST.SwinTransformer3D(**c["vst"])
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    ck = GC.synth_swin2d_checkpoint(shapes, c["seed"])
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "swin2d.pth")
+        torch.save(ck, path)
+        m.pretrained = path
+        m.inflate_weights(lambda *a: None)
+    sd = m.state_dict()
+    out = {"v:" + k: sd[k] for k in ck["model"] if k in sd and "relative_position_index" not in k}
+    v2 = R.S2.SwinTransformerV2(**c["mel"])
+    shapes2 = {k: tuple(t.shape) for k, t in v2.state_dict().items()}
+    ck2 = GC.synth_swinv2_checkpoint(shapes2, c["seed"] + 1)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "swinv2.pth")
+        torch.save(ck2, path)
+        args = types.SimpleNamespace(audio_ckpt_path=path, audio_pretrained_dir=path)
+        import src.utils as RU
+        RU.load_pretrained(args, v2, lambda *a: None)
+    sd2 = v2.state_dict()
+    out.update({"a:" + k: sd2[k] for k in ck2["checkpoint"]})
+    save(c["name"], _big=4096, _sample=1024, **out)
+
+
 def case_mel_c2():
     """SwinV2-B mel stage-3 block pair (reference BasicLayer: W-MSA then SW-MSA shift 3)."""
     c = GC.MEL_C2_S3
@@ -383,6 +414,6 @@ if __name__ == "__main__":
     only = sys.argv[1:]
     for fn in [case_window_attention, case_block, case_patch_embed_merge, case_vst_c1, case_w2v, case_head,
                case_fused_c1, case_block_c2, case_mel_c2, case_fused_c1_grads, case_fused_c2, case_state_keys,
-               case_config_flags, case_inception, case_block_c4]:
+               case_config_flags, case_inception, case_block_c4, case_pretrained]:
         if not only or fn.__name__ in only:
             fn()
