@@ -23,7 +23,7 @@ def run(n):
     import torch
     import bench
     from deepfake_amd.models.fused import CONFIGS
-    fn, flops = bench.roofline_case(CONFIGS["c2"], 8, torch.bfloat16)
+    fn, flops, _ = bench.roofline_case(CONFIGS["c2"], 8, torch.bfloat16)
     for _ in range(n):
         fn()
     torch.cuda.synchronize()
