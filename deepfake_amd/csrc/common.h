@@ -195,3 +195,6 @@ static inline int dfk_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // weight-resident streaming GEMM (wres.hip): 1 = launched, 0 = not applicable, < 0 = launch error
 int dfk_wres_try(const dfk_gemm_args& g, hipStream_t s);
+int dfk_wgrad_try(const dfk_gemm_args& g, hipStream_t s);
+// zeroed arrival-ticket slice of n counters for an in-launch combine (gemm.hip), nullptr if unavailable
+uint32_t* dfk_ticket_slice(long n, hipStream_t s);

@@ -15,11 +15,20 @@
 // bf16 launches with plain views take the LDS-DMA kernel instead (gemm_dma_kernel, below): the same tiles
 // and MFMAs, operands moved HBM -> LDS by buffer_load ... lds with source-swizzled, conflict-free images.
 // The register-staged kernel remains for fp32 parity mode and the implicit-conv views.
+#include <mutex>
+
 #include "common.h"
 
 namespace {
 
 constexpr int NT = 256;   // 4 waves (2 x 2), wave tile WT x WT, workgroup tile 2WT x 2WT
+
+// split-K state of a launch: fp32 partial slabs [z][split][M][N] and (in-launch combine) one arrival ticket per
+// output tile; cnt == nullptr: the partials are combined by splitk_reduce_kernel instead
+struct SplitK {
+  float* slab;
+  uint32_t* cnt;
+};
 
 template <typename T> struct GT;
 template <> struct GT<bf16raw> { static constexpr int BK = 64, VEC = 8, PADR = 8, PADK = 16; };
@@ -236,12 +245,12 @@ __device__ __forceinline__ void epilogue8(const dfk_gemm_args& g, int z0, int z1
 template <typename T, int WT, bool MXO = false>
 __device__ __forceinline__ void tile_epilogue(const dfk_gemm_args& g, float* smem, const f32x4 (&acc)[WT / 16][WT / 16],
                                               int lane, int wave, int wm, int wn, int bm, int bn, int z, int split,
-                                              int evec, float* slab);
+                                              int tile, int evec, SplitK sk);
 __device__ __forceinline__ int mx_scale_byte(float am);
 __device__ __forceinline__ uint2 mx_pack8(const float (&v)[8], int e);
 
 template <typename T, int WT, bool AK, bool BKM, bool VECOK, bool CONV, bool RS = false>
-__global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int evec, float* slab) {
+__global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kchunk, int evec, SplitK sk) {
   constexpr int BM = 2 * WT, BN = 2 * WT, MI = WT / 16;
   constexpr int VA = tile_vecs<T, BM>(), VB = tile_vecs<T, BN>();
   using TA = Tile<T, AK, BM>;
@@ -374,7 +383,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
       }
   }
   __syncthreads();   // every wave is done reading the last k-tile before the staging overwrites it
-  tile_epilogue<T, WT>(g, reinterpret_cast<float*>(smem), acc, lane, wave, wm, wn, bm, bn, z, split, evec, slab);
+  tile_epilogue<T, WT>(g, reinterpret_cast<float*>(smem), acc, lane, wave, wm, wn, bm, bn, z, split,
+                       (z * (int)gridDim.y + tmi) * (int)gridDim.x + tn, evec, sk);
 }
 
 // Epilogue shared by the GEMM kernels: stage each wave's WT x WT fp32 tile through LDS (the 16x16 MFMA C/D
@@ -383,7 +393,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const dfk_gemm_args g, int kc
 template <typename T, int WT, bool MXO>
 __device__ __forceinline__ void tile_epilogue(const dfk_gemm_args& g, float* smem, const f32x4 (&acc)[WT / 16][WT / 16],
                                               int lane, int wave, int wm, int wn, int bm, int bn, int z, int split,
-                                              int evec, float* slab) {
+                                              int tile, int evec, SplitK sk) {
   constexpr int MI = WT / 16, ES = WT + 4;   // staging row stride (fp32)
   const int z0 = z / g.nz1, z1 = z % g.nz1;
   float* es = smem + wave * WT * ES;
@@ -398,15 +408,57 @@ __device__ __forceinline__ void tile_epilogue(const dfk_gemm_args& g, float* sme
   const T* res = g.residual ? reinterpret_cast<const T*>(g.residual) + z0 * g.rbs0 + z1 * g.rbs1 : nullptr;
   const long coff = z0 * g.cbs0 + z1 * g.cbs1;
   T* aux = g.aux ? reinterpret_cast<T*>(g.aux) + coff : nullptr;
-  if (slab) {
+  if (sk.slab) {
     // split-K partial: raw fp32 sums to this split's slab, one row per wave instruction
     constexpr int RPI = 64 / WT;   // rows per wave instruction
     const int cl = lane % WT, col = bn + wn * WT + cl;
-    float* S = slab + ((long)(z * g.splitk + split) * g.M) * g.N;
+    const long MN = (long)g.M * g.N;
+    float* S = sk.slab + (long)(z * g.splitk + split) * MN;
 #pragma unroll 4
     for (int rl = lane / WT; rl < WT; rl += RPI) {
       const int row = bm + wm * WT + rl;
       if (row < g.M && col < g.N) S[(long)row * g.N + col] = es[rl * ES + cl];
+    }
+    if (!sk.cnt) return;   // splitk_reduce_kernel combines
+    // in-launch combine: publish the slab (drain, barrier, one agent-scope release), draw a ticket; the tile's
+    // last arriver acquires, sums the splits and runs the epilogue.  "Last" is broadcast through the kernel's one
+    // LDS array (every wave has finished reading its staging tile at the barrier).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t t = __hip_atomic_fetch_add(sk.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = t == (uint32_t)(g.splitk - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(sk.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // the slice's next use
+      }
+      smem[0] = last ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (smem[0] == 0.f) return;
+    // splits summed in split order (as splitk_reduce_kernel), 8 columns per lane of this wave's WT x WT part
+    constexpr int CPR = WT / 8;
+    const float* S0 = sk.slab + (long)z * g.splitk * MN;
+    for (int it = lane; it < WT * CPR; it += 64) {
+      const int row = bm + wm * WT + it / CPR, col0 = bn + wn * WT + (it % CPR) * 8;
+      if (row >= g.M || col0 >= g.N) continue;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const int ncol = min(8, g.N - col0);
+      const bool vec = (g.N % 4) == 0 && ncol == 8;
+      const float* src = S0 + (long)row * g.N + col0;
+      for (int sidx = 0; sidx < g.splitk; ++sidx, src += MN) {
+        if (vec) {
+          const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+          v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
+          v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
+        } else {
+          for (int e = 0; e < 8; ++e) if (e < ncol) v[e] += src[e];
+        }
+      }
+      epilogue8<T>(g, z0, z1, row, col0, v, evec);
     }
     return;
   }
@@ -567,7 +619,7 @@ __host__ __device__ __forceinline__ long view_extent(const dfk_view& v, long row
 // 1.5x the staged bytes, so one DMA in flight covers more of its latency).
 template <int WT, int NWM, int NWN, bool AK, bool BKM, int S, bool RS, bool CONV = false>
 __global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm_args g, int kchunk, int evec,
-                                                                  float* slab) {
+                                                                  SplitK sk) {
   constexpr int NWV = NWM * NWN, BM = NWM * WT, BN = NWN * WT, MI = WT / 16, BK = 64;
   constexpr int STAGE = (BM + BN) * BK;                         // elements per LDS stage
   constexpr int ES = WT + 4;
@@ -670,7 +722,8 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  tile_epilogue<bf16raw, WT>(g, smem_f, acc, lane, wave, wm, wn, bm, bn, z, split, evec, slab);
+  tile_epilogue<bf16raw, WT>(g, smem_f, acc, lane, wave, wm, wn, bm, bn, z, split,
+                             (z * (int)gridDim.y + tmi) * (int)gridDim.x + tn, evec, sk);
 }
 
 // split-K slabs [z][split][M][N] fp32 -> sum -> epilogue (8 columns per thread)
@@ -720,47 +773,47 @@ bool view_vec(const dfk_view& v, int vec) {
 }
 
 template <typename T, int WT, bool VECOK, bool CONV>
-void dispatch_wt(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+void dispatch_wt(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, SplitK sk, hipStream_t s) {
   if (g.a_kmajor) {
     if (g.b_kmajor) {
-      if (g.rowsum) hipLaunchKernelGGL((gemm_kernel<T, WT, true, true, VECOK, CONV, true>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
-      else hipLaunchKernelGGL((gemm_kernel<T, WT, true, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+      if (g.rowsum) hipLaunchKernelGGL((gemm_kernel<T, WT, true, true, VECOK, CONV, true>), grid, dim3(NT), 0, s, g, kchunk, evec, sk);
+      else hipLaunchKernelGGL((gemm_kernel<T, WT, true, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, sk);
     }
-    else hipLaunchKernelGGL((gemm_kernel<T, WT, true, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_kernel<T, WT, true, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, sk);
   } else {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, WT, false, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
-    else hipLaunchKernelGGL((gemm_kernel<T, WT, false, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, slab);
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_kernel<T, WT, false, true, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, sk);
+    else hipLaunchKernelGGL((gemm_kernel<T, WT, false, false, VECOK, CONV>), grid, dim3(NT), 0, s, g, kchunk, evec, sk);
   }
 }
 
 // implicit-conv views (wav2vec2 conv1-6 and their weight gradients): 2 LDS stages, 64x64 / 128x128 tiles
 template <int WT>
-void dispatch_dma_conv(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+void dispatch_dma_conv(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, SplitK sk, hipStream_t s) {
   const dim3 blk(256);
   if (g.a_kmajor) {
     if (g.b_kmajor) {
-      if (g.rowsum) hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, true, true, 2, true, true>), grid, blk, 0, s, g, kchunk, evec, slab);
-      else hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, true, true, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, slab);
+      if (g.rowsum) hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, true, true, 2, true, true>), grid, blk, 0, s, g, kchunk, evec, sk);
+      else hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, true, true, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, sk);
     }
-    else hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, true, false, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, true, false, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, sk);
   } else {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, false, true, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, slab);
-    else hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, false, false, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, slab);
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, false, true, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, sk);
+    else hipLaunchKernelGGL((gemm_dma_kernel<WT, 2, 2, false, false, 2, false, true>), grid, blk, 0, s, g, kchunk, evec, sk);
   }
 }
 
 template <int WT, int NWM, int NWN, int S>
-void dispatch_dma_s(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+void dispatch_dma_s(const dfk_gemm_args& g, dim3 grid, int kchunk, int evec, SplitK sk, hipStream_t s) {
   const dim3 blk(NWM * NWN * 64);
   if (g.a_kmajor) {
     if (g.b_kmajor) {
-      if (g.rowsum) hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, true, true, S, true>), grid, blk, 0, s, g, kchunk, evec, slab);
-      else hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, true, true, S, false>), grid, blk, 0, s, g, kchunk, evec, slab);
+      if (g.rowsum) hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, true, true, S, true>), grid, blk, 0, s, g, kchunk, evec, sk);
+      else hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, true, true, S, false>), grid, blk, 0, s, g, kchunk, evec, sk);
     }
-    else hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, true, false, S, false>), grid, blk, 0, s, g, kchunk, evec, slab);
+    else hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, true, false, S, false>), grid, blk, 0, s, g, kchunk, evec, sk);
   } else {
-    if (g.b_kmajor) hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, false, true, S, false>), grid, blk, 0, s, g, kchunk, evec, slab);
-    else hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, false, false, S, false>), grid, blk, 0, s, g, kchunk, evec, slab);
+    if (g.b_kmajor) hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, false, true, S, false>), grid, blk, 0, s, g, kchunk, evec, sk);
+    else hipLaunchKernelGGL((gemm_dma_kernel<WT, NWM, NWN, false, false, S, false>), grid, blk, 0, s, g, kchunk, evec, sk);
   }
 }
 
@@ -775,23 +828,23 @@ int dma_stages(int wt) {
 }
 
 // wt: 32 -> 64x64 tiles, 64 -> 128x128, 128 -> 256x128 (8 waves)
-void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
+void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, SplitK sk, hipStream_t s) {
   if (g.a.conv_cg > 0 || g.b.conv_cg > 0) {
-    if (wt == 32) dispatch_dma_conv<32>(g, grid, kchunk, evec, slab, s);
-    else dispatch_dma_conv<64>(g, grid, kchunk, evec, slab, s);
+    if (wt == 32) dispatch_dma_conv<32>(g, grid, kchunk, evec, sk, s);
+    else dispatch_dma_conv<64>(g, grid, kchunk, evec, sk, s);
     return;
   }
   const int st = dma_stages(wt);
   if (wt == 128) {
-    if (st == 3) dispatch_dma_s<64, 4, 2, 3>(g, grid, kchunk, evec, slab, s);
-    else dispatch_dma_s<64, 4, 2, 2>(g, grid, kchunk, evec, slab, s);
+    if (st == 3) dispatch_dma_s<64, 4, 2, 3>(g, grid, kchunk, evec, sk, s);
+    else dispatch_dma_s<64, 4, 2, 2>(g, grid, kchunk, evec, sk, s);
   } else if (wt == 64) {
-    if (st == 2) dispatch_dma_s<64, 2, 2, 2>(g, grid, kchunk, evec, slab, s);
-    else dispatch_dma_s<64, 2, 2, 3>(g, grid, kchunk, evec, slab, s);
+    if (st == 2) dispatch_dma_s<64, 2, 2, 2>(g, grid, kchunk, evec, sk, s);
+    else dispatch_dma_s<64, 2, 2, 3>(g, grid, kchunk, evec, sk, s);
   } else {
-    if (st == 2) dispatch_dma_s<32, 2, 2, 2>(g, grid, kchunk, evec, slab, s);
-    else if (st == 4) dispatch_dma_s<32, 2, 2, 4>(g, grid, kchunk, evec, slab, s);
-    else dispatch_dma_s<32, 2, 2, 3>(g, grid, kchunk, evec, slab, s);
+    if (st == 2) dispatch_dma_s<32, 2, 2, 2>(g, grid, kchunk, evec, sk, s);
+    else if (st == 4) dispatch_dma_s<32, 2, 2, 4>(g, grid, kchunk, evec, sk, s);
+    else dispatch_dma_s<32, 2, 2, 3>(g, grid, kchunk, evec, sk, s);
   }
 }
 
@@ -805,9 +858,9 @@ bool dma_ok(const dfk_gemm_args& g) {
 }
 
 template <typename T, bool VECOK, bool CONV>
-void dispatch(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, float* slab, hipStream_t s) {
-  if (wt == 32) dispatch_wt<T, 32, VECOK, CONV>(g, grid, kchunk, evec, slab, s);
-  else dispatch_wt<T, 64, VECOK, CONV>(g, grid, kchunk, evec, slab, s);
+void dispatch(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, SplitK sk, hipStream_t s) {
+  if (wt == 32) dispatch_wt<T, 32, VECOK, CONV>(g, grid, kchunk, evec, sk, s);
+  else dispatch_wt<T, 64, VECOK, CONV>(g, grid, kchunk, evec, sk, s);
 }
 
 // wave tile: 64 (128 x 128 workgroup tiles) unless that grid has fewer than eight tiles per CU: then 32
@@ -847,6 +900,7 @@ int auto_splitk(const dfk_gemm_args& g) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+
 template <typename T>
 int launch(const dfk_gemm_args& g, hipStream_t s) {
   constexpr int VEC = GT<T>::VEC, TBK = GT<T>::BK;
@@ -863,6 +917,8 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
     const int w = dfk_wres_try(g, s);     // huge-M / small-weight Linears: weight-resident streaming kernel
     if (w != 0) return w > 0 ? 0 : w;
+    const int d = dfk_wgrad_try(g, s);    // their weight gradients: token-streaming, output slice in registers
+    if (d != 0) return d > 0 ? 0 : d;
   }
   // split-K through fp32 slabs + a reduce/epilogue kernel: caller-chosen (splitk > 1, no atomics) or
   // automatic for grids too small to fill the chip
@@ -890,14 +946,15 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
                     (!g.residual || (aligned16(g.residual) && g.ldr % 8 == 0 && g.rbs0 % 8 == 0 && g.rbs1 % 8 == 0)) &&
                     (!g.aux || (aligned16(g.aux) && g.ldaux % 8 == 0));
   float* slab = autos > 1 ? reinterpret_cast<float*>(g.ws) : nullptr;
+  const SplitK sk{slab, slab ? dfk_ticket_slice((long)grid.x * grid.y * g.nz0 * g.nz1, s) : nullptr};
   if (vec) {
-    if (dma) dispatch_dma(gg, wt, grid, kchunk, evec, slab, s);
-    else if (conv) dispatch<T, true, true>(gg, wt, grid, kchunk, evec, slab, s);
-    else dispatch<T, true, false>(gg, wt, grid, kchunk, evec, slab, s);
+    if (dma) dispatch_dma(gg, wt, grid, kchunk, evec, sk, s);
+    else if (conv) dispatch<T, true, true>(gg, wt, grid, kchunk, evec, sk, s);
+    else dispatch<T, true, false>(gg, wt, grid, kchunk, evec, sk, s);
   } else {
-    dispatch<T, false, true>(gg, wt, grid, kchunk, evec, slab, s);
+    dispatch<T, false, true>(gg, wt, grid, kchunk, evec, sk, s);
   }
-  if (slab) {
+  if (slab && !sk.cnt) {   // no ticket arena: the reduce / epilogue launch combines the splits
     const long threads = (long)g.nz0 * g.nz1 * g.M * dfk_cdiv(g.N, 8);
     hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3((unsigned)dfk_cdiv(threads, 256)), dim3(256), 0, s, g, slab,
                        autos, evec ? 1 : 0);
@@ -1038,7 +1095,7 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_mx_kernel(const dfk_gemm_
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  tile_epilogue<bf16raw, WT, MXO>(g, smem_f, acc, lane, wave, wm, wn, bm, bn, 0, 0, evec, nullptr);
+  tile_epilogue<bf16raw, WT, MXO>(g, smem_f, acc, lane, wave, wm, wn, bm, bn, 0, 0, 0, evec, SplitK{nullptr, nullptr});
 }
 
 // ---- MX quantisation (dfk_mx_quant) ----
@@ -1137,6 +1194,39 @@ bool epi_vec(const dfk_gemm_args& g) {
 }
 
 }  // namespace
+
+// Arrival tickets of the in-launch split-K combine: one zeroed arena of counters per device, handed out in
+// consecutive slices (a launch's tiles), round robin.  Every ticket returns to 0 when its tile's last arriver
+// resets it, so a slice is zero whenever it is handed out again; launches that can run concurrently (other
+// streams, one captured graph) hold disjoint slices as long as fewer than kTickets tiles are in flight.
+// nullptr: no arena (first use inside a stream capture, or allocation failure): the caller combines in a
+// separate launch (splitk_reduce_kernel, slab_colsum).  Shared by the GEMM split-K and LayerNorm dγ/dβ partials.
+constexpr long kTickets = 1L << 20;
+uint32_t* dfk_ticket_slice(long n, hipStream_t s) {
+  static const bool off = getenv("DFK_INLAUNCH_COMBINE") && atoi(getenv("DFK_INLAUNCH_COMBINE")) == 0;   // A/B
+  if (off || n <= 0 || n > kTickets) return nullptr;
+  static std::mutex mu;
+  static uint32_t* arena[64] = {};
+  static long cursor[64] = {};
+  std::lock_guard<std::mutex> lock(mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!arena[dev]) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, kTickets * 4) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, kTickets * 4, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    arena[dev] = static_cast<uint32_t*>(p);
+  }
+  if (cursor[dev] + n > kTickets) cursor[dev] = 0;
+  uint32_t* t = arena[dev] + cursor[dev];
+  cursor[dev] += (n + 63) & ~63L;
+  return t;
+}
 
 extern "C" int dfk_gemm(const dfk_gemm_args* g, hipStream_t s) {
   if (!g || g->mx_q) return DFK_EINVAL;   // the MX copy of C is a dfk_gemm_mx epilogue

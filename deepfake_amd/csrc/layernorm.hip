@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
                                               const T* __restrict__ w, const float* __restrict__ mean,
                                               const float* __restrict__ rstd, T* __restrict__ dx, float* dw,
                                               float* db, long rows, int C, int accumulate, float* __restrict__ part,
-                                              const dfk_drop drop) {
+                                              const dfk_drop drop, uint32_t* cnt, int gs) {
   constexpr int RPW = 64 / L;
   constexpr bool KEEP = V <= 4;   // x, dy stay in registers between the two sweeps
   extern __shared__ float red[];  // [2][C] block partials of dw, db
@@ -222,8 +222,40 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
     }
     __syncthreads();
   }
-  if (part) {   // block partials -> [blocks][2C] slab, summed by a column-sum pass (no same-address atomics)
+  if (part) {   // block partials -> [blocks][2C] slab (no same-address atomics from every block)
     for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) part[(long)blockIdx.x * 2 * C + i] = red[i];
+    if (!cnt) return;   // slab_colsum sums the slab
+    // in-launch combine per group of gs blocks: publish (drain, barrier, agent release), ticket; the group's last
+    // arriver acquires, sums the group's rows in block order and adds the group sum (groups-way atomics)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int grp = blockIdx.x / gs, g0 = grp * gs, gn = min(gs, (int)gridDim.x - g0);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t t = __hip_atomic_fetch_add(cnt + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = t == (uint32_t)(gn - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(cnt + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      red[0] = last ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (red[0] == 0.f) return;
+    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) {
+      const float* src = part + (long)g0 * 2 * C + i;
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      int r = 0;
+      for (; r + 8 <= gn; r += 8)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] += src[(long)(r + u) * 2 * C];
+      for (; r < gn; ++r) a[0] += src[(long)r * 2 * C];   // ragged last group
+      const float t = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+      float* out = i < C ? dw : db;
+      if (out) atomicAdd(out + (i < C ? i : i - C), t);
+    }
     return;
   }
   for (int i = threadIdx.x; i < C; i += blockDim.x) {
@@ -278,9 +310,13 @@ void bwd_launch(const void* dy, const void* x, const void* w, const float* mean,
                 float* db, long rows, int C, int accumulate, float* ws, dfk_drop drop, hipStream_t s) {
   const int blocks = (int)bwd_blocks(rows, C);
   float* part = ws && (dw || db) ? ws : nullptr;
+  // in-launch combine groups: about 48 KB of partials per group's reducer, 8-64 blocks
+  int gs = 64;
+  while (gs > 8 && (long)gs * 8 * C > 49152) gs >>= 1;
+  uint32_t* cnt = part ? dfk_ticket_slice(dfk_cdiv(blocks, gs), s) : nullptr;
   hipLaunchKernelGGL((ln_bwd<T, L, V>), dim3(blocks), dim3(256), 2 * C * sizeof(float), s, (const T*)dy,
-                     (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part, drop);
-  if (part)
+                     (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part, drop, cnt, gs);
+  if (part && !cnt)
     hipLaunchKernelGGL(slab_colsum, dim3(dfk_cdiv(2 * C, 64), dfk_cdiv(blocks, 256)), dim3(256), 0, s, part, blocks, C,
                        dw, db);
 }

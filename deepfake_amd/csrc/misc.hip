@@ -142,6 +142,9 @@ __global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, long n
 
 // torch.optim.SGD semantics (momentum, dampening 0, weight decay, no nesterov):
 //   g = grad + wd*p ; buf = first ? g : mom*buf + g ; p -= lr*buf ; shadow = bf16(p)
+// NT: the parameter / momentum / shadow stores are non-temporal (streamed to HBM, not left dirty in L2 / MALL),
+// so that their write-back does not land on the first kernels of the next step (the clip-batch patch embedding)
+template <bool NT>
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ grad, float* __restrict__ buf,
                            bf16raw* __restrict__ shadow, long n, const float* __restrict__ lr_dev, float lr_host,
                            float mom, float wd, int first, const float* __restrict__ gate) {
@@ -162,14 +165,21 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ grad
       bb[k] = first ? g : mom * bb[k] + g;
       pp[k] -= lr * bb[k];
     }
-    *reinterpret_cast<float4*>(p + i0) = pv;
-    *reinterpret_cast<float4*>(buf + i0) = bv;
+    if constexpr (NT) {
+      __builtin_nontemporal_store(__builtin_bit_cast(f32x4, pv), reinterpret_cast<f32x4*>(p + i0));
+      __builtin_nontemporal_store(__builtin_bit_cast(f32x4, bv), reinterpret_cast<f32x4*>(buf + i0));
+    } else {
+      *reinterpret_cast<float4*>(p + i0) = pv;
+      *reinterpret_cast<float4*>(buf + i0) = bv;
+    }
     if (shadow) {
       uint2 u;
       bf16raw* e = reinterpret_cast<bf16raw*>(&u);
 #pragma unroll
       for (int k = 0; k < 4; ++k) e[k] = f2bf(pp[k]);
-      *reinterpret_cast<uint2*>(shadow + i0) = u;
+      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+      if constexpr (NT) __builtin_nontemporal_store(__builtin_bit_cast(u32x2, u), reinterpret_cast<u32x2*>(shadow + i0));
+      else *reinterpret_cast<uint2*>(shadow + i0) = u;
     }
   } else {
     for (long i = i0; i < n; ++i) {
@@ -420,7 +430,9 @@ extern "C" int dfk_sgd_step(float* param, const float* grad, float* momentum_buf
     return DFK_EINVAL;
   if (n <= 0) return 0;
   const long threads = (n + 3) / 4;
-  hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, param, grad, momentum_buf,
+  static const bool nt = !getenv("DFK_SGD_NT") || atoi(getenv("DFK_SGD_NT")) != 0;   // 0: plain stores (A/B runs)
+  auto kfn = nt ? sgd_kernel<true> : sgd_kernel<false>;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, param, grad, momentum_buf,
                      (bf16raw*)bf16_shadow, (long)n, lr_dev, lr, momentum, weight_decay, first_step, gate);
   DFK_CHECK_LAUNCH();
   return 0;

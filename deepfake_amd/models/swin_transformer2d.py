@@ -33,7 +33,13 @@ class Mlp(nn.Module):
         self.fc1 = nn.Linear(in_features, hidden_features)
         self.act = act_layer()
         self.fc2 = nn.Linear(hidden_features, out_features)
-        self.drop = nn.Dropout(drop)
+        self.drop = nn.Dropout(drop)   # module tree parity; the masks are the two device sites below
+        self.sites = (rng.Drop(drop), rng.Drop(drop)) if drop > 0 else None   # after the GELU, after fc2
+
+    def drop_specs(self):
+        if self.sites is None or not self.training:
+            return None, None
+        return self.sites[0].spec(), self.sites[1].spec()
 
 
 def window_partition(x, window_size):
@@ -56,8 +62,10 @@ class WindowAttention(nn.Module):
     def __init__(self, dim, window_size, num_heads, qkv_bias=True, attn_drop=0., proj_drop=0.,
                  pretrained_window_size=[0, 0]):
         super().__init__()
-        if attn_drop or proj_drop:
-            raise NotImplementedError("attention/proj dropout > 0")
+        # attn_drop (:176, softmax probabilities, in the attention kernel) and proj_drop (:182, proj epilogue)
+        # as device dropout sites, created only when p > 0
+        self.attn_drop = rng.Drop(attn_drop) if attn_drop > 0 else None
+        self.proj_drop = rng.Drop(proj_drop) if proj_drop > 0 else None
         self.dim, self.window_size, self.pretrained_window_size = dim, window_size, pretrained_window_size
         self.num_heads = num_heads
         self.logit_scale = nn.Parameter(torch.log(10 * torch.ones((num_heads, 1, 1))), requires_grad=True)
@@ -111,7 +119,8 @@ class WindowAttention(nn.Module):
         qkv = Fn.CosineQKFn.apply(qkv, self.logit_scale, self.num_heads, hd, math.log(1. / 0.01))
         geo = (dims, (1, ws, ws), (1, self.window_size[0], self.window_size[1]), (0, shift, shift),
                self.num_heads, hd, 1.0)
-        out = Fn.window_attention(qkv, self.bias_table(), None, geo)
+        ad = self.attn_drop.spec() if self.attn_drop is not None and self.training else None
+        out = Fn.window_attention(qkv, self.bias_table(), None, geo, drop=ad)
         return (out, xs) if skip else out
 
 
@@ -122,8 +131,6 @@ class SwinTransformerBlock(nn.Module):
                  drop=0., attn_drop=0., drop_path=0., act_layer=nn.GELU, norm_layer=nn.LayerNorm,
                  pretrained_window_size=0):
         super().__init__()
-        if drop > 0:
-            raise NotImplementedError("dropout > 0 in the SwinV2 block is not implemented on the MI355X path")
         self.dim, self.input_resolution, self.num_heads = dim, input_resolution, num_heads
         self.window_size, self.shift_size, self.mlp_ratio = window_size, shift_size, mlp_ratio
         if min(self.input_resolution) <= self.window_size:
@@ -160,11 +167,14 @@ class SwinTransformerBlock(nn.Module):
         assert L == H * W, "input feature has wrong size"
         x2 = x.reshape(-1, C)
         a, x2s = self.attn.core(x2, (B, 1, H, W), self.window_size, self.shift_size, skip=True)
-        a = Fn.linear(a, self.attn.proj.weight, self.attn.proj.bias)
+        pd = self.attn.proj_drop.spec() if self.attn.proj_drop is not None and self.training else None
+        a = Fn.linear(a, self.attn.proj.weight, self.attn.proj.bias, drop=pd)
         on = self.dp is not None and self.training
         dp = (self.dp[0].spec(L), self.dp[1].spec(L)) if on else (None, None)
         x2 = Fn.layer_norm(a, self.norm1, residual=x2s, drop=dp[0])   # x + DropPath(LN(attn)) (:301)
-        m, x2s = Fn.mlp(x2, self.mlp.fc1, self.mlp.fc2, skip=True)   # x2's residual gradient joins fc1's dX
+        da, do = self.mlp.drop_specs()
+        m, x2s = Fn.mlp(x2, self.mlp.fc1, self.mlp.fc2, skip=True, drop_act=da, drop_out=do)   # x2's residual
+        # gradient joins fc1's dX
         x2 = Fn.layer_norm(m, self.norm2, residual=x2s, drop=dp[1])   # x + DropPath(LN(mlp)) (:304)
         return x2.view(B, L, C)
 

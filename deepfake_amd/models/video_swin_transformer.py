@@ -84,9 +84,11 @@ class WindowAttention3D(nn.Module):
 
     def __init__(self, dim, window_size, num_heads, qkv_bias=False, qk_scale=None, attn_drop=0., proj_drop=0.):
         super().__init__()
-        if attn_drop or proj_drop:
-            raise NotImplementedError("attention/proj dropout > 0 is not implemented on the MI355X path")
         self.dim, self.window_size, self.num_heads = dim, tuple(window_size), num_heads
+        # attn_drop (:165, on the softmax probabilities: the attention kernels' DROP variants) and proj_drop
+        # (:171, the proj GEMM epilogue) as device dropout sites, created only when p > 0
+        self.attn_drop = rng.Drop(attn_drop) if attn_drop > 0 else None
+        self.proj_drop = rng.Drop(proj_drop) if proj_drop > 0 else None
         head_dim = dim // num_heads
         self.scale = qk_scale or head_dim ** -0.5
         L = (2 * window_size[0] - 1) * (2 * window_size[1] - 1) * (2 * window_size[2] - 1)
@@ -96,20 +98,26 @@ class WindowAttention3D(nn.Module):
         self.proj = nn.Linear(dim, dim)
         nn.init.trunc_normal_(self.relative_position_bias_table, std=.02)
 
+    def drop_specs(self):
+        """(attention-probability, proj-output) dropout specs; None outside training or at p = 0."""
+        on = lambda d: d.spec() if d is not None and self.training else None   # noqa: E731
+        return on(self.attn_drop), on(self.proj_drop)
+
     def core(self, qkv, dims, window, shift, mask=None):
-        """Attention core over a token-major qkv buffer; returns [rows, C] (pre-proj)."""
+        """Attention core over a token-major qkv buffer; returns [rows, C] (pre-proj).  Attention dropout
+        (training, attn_drop > 0) masks P in the kernel: unit (window, head) row q col k of the mask stream."""
         hd = self.dim // self.num_heads
         geo = (tuple(dims), tuple(window), self.window_size, tuple(shift), self.num_heads, hd, self.scale)
         padded = any(n % w for n, w in zip(dims[1:], window))
         return Fn.window_attention(qkv, self.relative_position_bias_table,
-                                   self.qkv.bias if padded else None, geo, mask)
+                                   self.qkv.bias if padded else None, geo, mask, drop=self.drop_specs()[0])
 
     def forward(self, x, mask=None):
         B_, N, C = x.shape
         qkv = Fn.linear(x.reshape(-1, C), self.qkv.weight, self.qkv.bias)
         m = mask.float().contiguous() if mask is not None else None
         o = self.core(qkv, (B_, 1, 1, N), (1, 1, N), (0, 0, 0), mask=m)
-        return Fn.linear(o, self.proj.weight, self.proj.bias).view(B_, N, C)
+        return Fn.linear(o, self.proj.weight, self.proj.bias, drop=self.drop_specs()[1]).view(B_, N, C)
 
 
 class SwinTransformerBlock3D(nn.Module):
@@ -121,8 +129,6 @@ class SwinTransformerBlock3D(nn.Module):
                  qk_scale=None, drop=0., attn_drop=0., drop_path=0., act_layer=nn.GELU, norm_layer=nn.LayerNorm,
                  use_checkpoint=False):
         super().__init__()
-        if drop > 0:
-            raise NotImplementedError("dropout > 0 in the Swin3D block is not implemented on the MI355X path")
         self.dim, self.num_heads = dim, num_heads
         self.window_size, self.shift_size = tuple(window_size), tuple(shift_size)
         self.mlp_ratio, self.use_checkpoint = mlp_ratio, use_checkpoint
@@ -150,18 +156,29 @@ class SwinTransformerBlock3D(nn.Module):
         return self._part1(Fn.layer_norm(x, self.norm1), x.shape[:4])
 
     def _attn_branch(self, x, dp):
-        """x + DropPath(proj(W-MSA(LN1 x)))  (forward_part1 + the first residual, :266-271).  The residual
-        reads LN1's skip alias of x, so x's two gradients meet inside the LN backward."""
+        """x + DropPath(proj_drop(proj(W-MSA(LN1 x))))  (forward_part1 + the first residual, :266-271).  The
+        residual reads LN1's skip alias of x, so x's two gradients meet inside the LN backward.  One dropout
+        runs in the proj epilogue; with both proj_drop and DropPath active the DropPath is a separate pass."""
         B, D, H, W, C = x.shape
         xn, xs = Fn.layer_norm(x, self.norm1, skip=True)
         o = self._part1(xn, (B, D, H, W))
+        pd = self.attn.drop_specs()[1]
+        if pd is not None and dp is not None:
+            z = Fn.linear(o, self.attn.proj.weight, self.attn.proj.bias, drop=pd, mx=self.mx)
+            return (xs.reshape(-1, C) + Fn.DropoutFn.apply(z, dp)).view(B, D, H, W, C)
         return Fn.linear(o, self.attn.proj.weight, self.attn.proj.bias, residual=xs.reshape(-1, C),
-                         drop=dp, mx=self.mx).view(B, D, H, W, C)
+                         drop=dp if pd is None else pd, mx=self.mx).view(B, D, H, W, C)
 
     def _mlp_branch(self, x, dp):
-        """x + DropPath(mlp(LN2 x))  (forward_part2 + the second residual, :273-276)."""
+        """x + DropPath(mlp(LN2 x))  (forward_part2 + the second residual, :273-276); Mlp's two dropouts
+        (after the GELU, after fc2) in the fc1 / fc2 epilogues."""
         xn, xs = Fn.layer_norm(x, self.norm2, skip=True)
-        return Fn.mlp(xn, self.mlp.fc1, self.mlp.fc2, residual=xs, drop_out=dp, mx=self.mx)
+        da, do = self.mlp.drop_specs()
+        if do is not None and dp is not None:
+            m = Fn.mlp(xn, self.mlp.fc1, self.mlp.fc2, drop_act=da, drop_out=do, mx=self.mx)
+            return xs + Fn.DropoutFn.apply(m.reshape(-1, xs.shape[-1]), dp).view(xs.shape)
+        return Fn.mlp(xn, self.mlp.fc1, self.mlp.fc2, residual=xs, drop_act=da, drop_out=dp if do is None else do,
+                      mx=self.mx)
 
     def forward(self, x, mask_matrix=None):
         B, D, H, W, C = x.shape

@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 
 from . import functional as Fn
+from . import rng
 
 
 class Mlp(nn.Module):
@@ -24,16 +25,22 @@ class Mlp(nn.Module):
         self.fc1 = nn.Linear(in_features, hidden_features)
         self.act = act_layer()
         self.fc2 = nn.Linear(hidden_features, out_features)
-        self.drop = nn.Dropout(drop)
+        self.drop = nn.Dropout(drop)   # module tree / state_dict parity; the masks are the sites below
         self.p = drop
+        # nn.Dropout is called twice per forward (after the GELU, after fc2): two independent draws, i.e. two
+        # device dropout sites, fused into the fc1 and fc2 GEMM epilogues (created only when p > 0, so the site
+        # numbering of dropout-free models is unchanged)
+        self.sites = (rng.Drop(drop), rng.Drop(drop)) if drop > 0 else None
+
+    def drop_specs(self):
+        """(after-GELU, after-fc2) dropout specs, or (None, None) outside training / at p = 0."""
+        if self.sites is None or not self.training:
+            return None, None
+        return self.sites[0].spec(), self.sites[1].spec()
 
     def forward(self, x, residual=None):
-        if self.p > 0 and self.training:
-            h = Fn.linear(x, self.fc1.weight, self.fc1.bias, act=1)
-            h = self.drop(h)
-            y = self.drop(Fn.linear(h, self.fc2.weight, self.fc2.bias))
-            return y if residual is None else y + residual
-        return Fn.mlp(x, self.fc1, self.fc2, residual=residual)
+        da, do = self.drop_specs()
+        return Fn.mlp(x, self.fc1, self.fc2, residual=residual, drop_act=da, drop_out=do)
 
 
 class AverageMeter:

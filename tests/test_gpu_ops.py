@@ -81,8 +81,33 @@ def test_linear_weight_resident(M, N, Kd):
     assert rel(K.linear_dx(dy, w, act=2, aux=aux2), ref2) < tol(dt)
 
 
+@pytest.mark.parametrize("M,N,Kd", [(20000, 288, 96), (16500, 96, 96), (17000, 384, 96), (16400, 96, 384),
+                                    (16385, 576, 192), (16384, 192, 768), (20000, 384, 128), (20000, 512, 128),
+                                    (16384, 128, 512), (16448, 128, 128), (16400, 384, 768)])
+def test_linear_dw_token_streaming(M, N, Kd):
+    """bf16 weight gradients with >= 16k tokens and a small dW run on the token-streaming kernel (wgrad.hip):
+    every instantiated wave grid, row / column slices (the bias gradient counted once per row), a ragged token
+    tail, accumulation into a non-zero dW, and an x that is a column view of a wider buffer (ld > Kd).
+    fp32 accumulation of exact bf16 products: checked at 1e-4 of the largest entry."""
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(3)
+    xb = torch.randn(M, Kd + 64, device=DEV, generator=g).to(dt)
+    x = xb[:, 32:32 + Kd]
+    dy = torch.randn(M, N, device=DEV, generator=g).to(dt)
+    dw0 = torch.randn(N, Kd, device=DEV, generator=g)
+    db0 = torch.randn(N, device=DEV, generator=g)
+    dw, db = dw0.clone(), db0.clone()
+    K.linear_dw(dy, x, dw, db=db)
+    ref = dw0.double() + dy.double().t() @ x.double()
+    assert rel(dw, ref) < 1e-4
+    assert rel(db, db0.double() + dy.double().sum(0)) < 1e-4
+    dw2 = torch.zeros(N, Kd, device=DEV)
+    K.linear_dw(dy, x, dw2)
+    assert rel(dw2, dy.double().t() @ x.double()) < 1e-4
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("rows,C", [(1000, 96), (33, 768), (17, 3072), (5, 512), (1001, 192), (77, 384), (9, 128),
+@pytest.mark.parametrize("rows,C",[(1000, 96), (33, 768), (17, 3072), (5, 512), (1001, 192), (77, 384), (9, 128),
                                     (13, 1536), (3, 1024), (29, 256)])
 def test_layernorm(dt, rows, C):
     g = torch.Generator(device=DEV).manual_seed(1)

@@ -128,7 +128,8 @@ def _w2v_attention_ref(qkv, B, T, heads, hd, m):
     return ((p * m) @ v).transpose(1, 2).reshape(B * T, C)
 
 
-@pytest.mark.parametrize("T,heads,hd", [(199, 12, 64), (49, 2, 64), (96, 3, 32)])
+@pytest.mark.parametrize("T,heads,hd", [(199, 12, 64), (49, 2, 64), (96, 3, 32),
+                                        (499, 2, 64)])   # Np 512: backward in query chunks, dK / dV accumulated
 def test_attention_dropout(T, heads, hd):
     """HF eager_attention_forward with attention dropout (:458): O = (softmax(QK^T s) * Z) V; the kernel's
     forward and all three input gradients against a torch fp32 reference using the kernel's own mask."""
@@ -290,3 +291,91 @@ def test_layerdrop_gate_is_or_over_accumulation_window():
                 assert rel(store.flat[s:e], want) < 1e-6, (i, rel(store.flat[s:e], want))
     store.zero_grad()
     assert torch.equal(enc.layer_used, torch.zeros_like(enc.layer_used))
+
+
+def _vst_block_ref(ob, x, z, pd, da, do, dp1, dp2):
+    """oracle/vst.py's Swin3D block (video_swin_transformer.py:142-173, 219-278) in fp32 with the kernels' own
+    masks injected: z on the softmax probabilities [windows, heads, N, N] (attn_drop, :165), pd on the proj
+    output (proj_drop, :171), da / do after the GELU and after fc2 (Mlp's nn.Dropout, src/utils.py:257-259), and
+    dp1 / dp2 the two DropPath draws; every token-row mask is indexed by the token's row b*DHW + (d*H + h)*W + w."""
+    import torch.nn.functional as F
+    from oracle.vst import clamp_window, shift_mask, window_token_index
+
+    B, D, H, W, C = x.shape
+    att = ob.attn
+    ws, ss = clamp_window((D, H, W), ob.window_size, ob.shift_size)
+    xn = F.layer_norm(x, (C,), ob.norm1.weight, ob.norm1.bias)
+    Dp, Hp, Wp = [-(-n // w) * w for n, w in zip((D, H, W), ws)]
+    xn = F.pad(xn, (0, 0, 0, Wp - W, 0, Hp - H, 0, Dp - D))
+    tok = window_token_index(Dp, Hp, Wp, ws).to(x.device)
+    d, h, w = tok // (Hp * Wp), (tok // Wp) % Hp, tok % Wp
+    src = (((d + ss[0]) % Dp) * Hp + (h + ss[1]) % Hp) * Wp + (w + ss[2]) % Wp
+    flat = xn.reshape(B, Dp * Hp * Wp, C)
+    win = flat[:, src.reshape(-1)].reshape(B * tok.shape[0], tok.shape[1], C)
+    B_, N = win.shape[:2]
+    nH, hd = att.num_heads, C // att.num_heads
+    qkv = att.qkv(win).view(B_, N, 3, nH, hd)
+    q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))
+    s = (q * hd ** -0.5) @ k.transpose(-1, -2)
+    bias = att.relative_position_bias_table[att.relative_position_index[:N, :N].reshape(-1)]
+    s = s + bias.view(N, N, nH).permute(2, 0, 1)[None]
+    if any(t > 0 for t in ss):
+        m = shift_mask(Dp, Hp, Wp, ws, ss).to(x.device)
+        s = (s.view(B_ // m.shape[0], m.shape[0], nH, N, N) + m[None, :, None]).view(B_, nH, N, N)
+    o = ((torch.softmax(s, dim=-1) * z) @ v).transpose(1, 2).reshape(B_, N, C)
+    y = att.proj(o).reshape(B, -1, C)
+    a = torch.zeros_like(flat).index_copy(1, src.reshape(-1), y).view(B, Dp, Hp, Wp, C)[:, :D, :H, :W]
+    x1 = x + (a.reshape(-1, C) * pd * dp1).view(B, D, H, W, C)
+    hmid = F.gelu(ob.mlp.fc1(F.layer_norm(x1, (C,), ob.norm2.weight, ob.norm2.bias))).reshape(-1, 4 * C) * da
+    return x1 + (ob.mlp.fc2(hmid) * do * dp2).view(B, D, H, W, C)
+
+
+@pytest.mark.parametrize("attn_drop,drop,drop_path", [(0.0, 0.0, 0.0), (0.15, 0.0, 0.0), (0.0, 0.1, 0.0), (0.0, 0.0, 0.2),
+                                                     (0.15, 0.1, 0.2)])
+def test_swin3d_block_dropouts(attn_drop, drop, drop_path):
+    """SwinTransformerBlock3D with attn_drop, drop (proj_drop and both Mlp dropouts) and drop_path > 0 (one at a
+    time, then all together), training mode, bf16: forward and every gradient against the fp32 reference block
+    using the kernels' masks (the attention mask row of (window w, head h, query q) is ((b nW + w) heads + h) Np + q,
+    key = column).  Eval mode ignores every dropout (equal to the same block built with p = 0)."""
+    import oracle.vst as OV
+    from oracle.fill import named_fill_, randn
+    import deepfake_amd.models.video_swin_transformer as V
+
+    C, heads, win, shift = 96, 3, (8, 7, 7), (4, 3, 3)
+    B, D, H, W = 2, 8, 14, 14
+    blk = named_fill_(V.SwinTransformerBlock3D(C, heads, window_size=win, shift_size=shift, drop=drop,
+                                               attn_drop=attn_drop, drop_path=drop_path), 5).to(DEV)
+    ob = named_fill_(OV.SwinTransformerBlock3D(C, heads, win, shift), 5).to(DEV)
+    x = randn(6, (B, D, H, W, C)).to(DEV)
+    blk.train()
+    xb = x.to(torch.bfloat16).requires_grad_(True)
+    y = blk(xb, None)
+    rows, nW, N, Np = B * D * H * W, 4, 392, 416
+    ones = lambda r, c: torch.ones(r, c, device=DEV)   # noqa: E731
+    z = (mask_of(blk.attn.attn_drop.spec(), B * nW * heads * Np, Np) if attn_drop else ones(B * nW * heads * Np, Np))
+    z = z.view(B * nW, heads, Np, Np)[:, :, :N, :N]
+    pd = mask_of(blk.attn.proj_drop.spec(), rows, C) if drop else ones(rows, C)
+    da = mask_of(blk.mlp.sites[0].spec(), rows, 4 * C) if drop else ones(rows, 4 * C)
+    do = mask_of(blk.mlp.sites[1].spec(), rows, C) if drop else ones(rows, C)
+    dp1 = mask_of(blk.dp[0].spec(D * H * W), rows, C) if drop_path else ones(rows, C)
+    dp2 = mask_of(blk.dp[1].spec(D * H * W), rows, C) if drop_path else ones(rows, C)
+    for mm, p in ((z, attn_drop), (pd, drop), (da, drop), (do, drop)):
+        assert abs((mm == 0).float().mean().item() - p) < 0.02
+    xf = xb.detach().float().requires_grad_(True)
+    ref = _vst_block_ref(ob, xf, z, pd, da, do, dp1, dp2)
+    ey = rel(y, ref)
+    dy = randn(7, y.shape).to(DEV).to(torch.bfloat16)
+    y.backward(dy)
+    ref.backward(dy.float())
+    ex = rel(xb.grad, xf.grad)
+    ours = dict(blk.named_parameters())
+    errs = {n: rel(ours[n].grad, p.grad) for n, p in ob.named_parameters()}
+    worst = max(errs.values())
+    print(f"dropout block ({attn_drop}, {drop}, {drop_path}): y {ey:.3e} dx {ex:.3e} parameter gradients "
+          + " ".join(f"{n} {e:.2e}" for n, e in errs.items()))
+    assert ey < 2e-2 and ex < 5e-2 and worst < 5e-2
+    # eval: no dropout anywhere
+    blk.eval()
+    ref0 = named_fill_(V.SwinTransformerBlock3D(C, heads, window_size=win, shift_size=shift), 5).to(DEV).eval()
+    with torch.no_grad():
+        assert torch.equal(blk(x.to(torch.bfloat16), None), ref0(x.to(torch.bfloat16), None))

@@ -114,7 +114,8 @@ def test_wattn_bwd(dt, case, table):
 
 def test_wattn_bwd_query_chunks():
     """A window whose Q / dO / dQ exceed the LDS (wav2vec2 at 10 s: T = 499, hd 64 -> Np 512) runs the backward
-    in query chunks, dK / dV accumulated across them (bf16, with attention dropout off and on)."""
+    in query chunks, dK / dV accumulated across them (bf16, attention dropout off; the dropout-on case of the
+    same geometry is test_gpu_regularize.py::test_attention_dropout[499-2-64])."""
     dims, window, fw, shift, heads, hd = (2, 1, 1, 499), (1, 1, 499), (1, 1, 499), (0, 0, 0), 2, 64
     g = torch.Generator(device=DEV).manual_seed(9)
     rows, C = 2 * 499, 2 * 64
