@@ -99,7 +99,7 @@ SIGNATURES = {
     "dfk_mx_quant": [_VP, C.c_int, _I64, _I64, _I64, C.c_int, _VP, _I64, _VP, _VP],
     "dfk_layernorm_fwd": [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, _F, C.c_int, _VP, C.POINTER(Drop), _VP],
     "dfk_layernorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, C.c_int, C.c_int, _VP,
-                          C.POINTER(Drop), _VP],
+                          C.POINTER(Drop), _VP, _VP],
     "dfk_layernorm_bwd_workspace": [_I64, _I32],
     "dfk_wattn_fwd": [C.POINTER(WattnArgs), _VP],
     "dfk_wattn_bwd": [C.POINTER(WattnBwdArgs), _VP],

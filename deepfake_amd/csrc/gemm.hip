@@ -1203,8 +1203,11 @@ bool epi_vec(const dfk_gemm_args& g) {
 // separate launch (splitk_reduce_kernel, slab_colsum).  Shared by the GEMM split-K and LayerNorm dγ/dβ partials.
 constexpr long kTickets = 1L << 20;
 uint32_t* dfk_ticket_slice(long n, hipStream_t s) {
-  static const bool off = getenv("DFK_INLAUNCH_COMBINE") && atoi(getenv("DFK_INLAUNCH_COMBINE")) == 0;   // A/B
-  if (off || n <= 0 || n > kTickets) return nullptr;
+  // opt-in (DFK_INLAUNCH_COMBINE=1): measured slower than the separate combine launch in the C2 step (the last
+  // arriver reads every split's slab serially: w2v dX 22 -> 43 us, LN backward 17 -> 45 us;
+  // profiles/gemm/r4o_inlaunch_combine_rejected.txt)
+  const char* env = getenv("DFK_INLAUNCH_COMBINE");   // read per call: tests switch it inside one process
+  if (!env || atoi(env) == 0 || n <= 0 || n > kTickets) return nullptr;
   static std::mutex mu;
   static uint32_t* arena[64] = {};
   static long cursor[64] = {};

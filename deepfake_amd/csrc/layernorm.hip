@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
                                               const T* __restrict__ w, const float* __restrict__ mean,
                                               const float* __restrict__ rstd, T* __restrict__ dx, float* dw,
                                               float* db, long rows, int C, int accumulate, float* __restrict__ part,
-                                              const dfk_drop drop, uint32_t* cnt, int gs) {
+                                              const dfk_drop drop, uint32_t* cnt, int gs, const T* __restrict__ addend) {
   constexpr int RPW = 64 / L;
   constexpr bool KEEP = V <= 4;   // x, dy stay in registers between the two sweeps
   extern __shared__ float red[];  // [2][C] block partials of dw, db
@@ -187,12 +187,14 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
         load8m<T>(dy, roff + vi * 8, ok, dv);
         dmask(dv, vi);
       }
-      if (accumulate) load8m<T>(dx, roff + vi * 8, ok, o);
+      const bool add = addend || accumulate;
+      if (addend) load8m<T>(addend, roff + vi * 8, ok, o);
+      else if (accumulate) load8m<T>(dx, roff + vi * 8, ok, o);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xh = (xv[e] - mu) * rs;
         const float d = rs * (dv[e] * wv[i][e] - m1 - xh * m2);
-        o[e] = accumulate ? o[e] + d : d;
+        o[e] = add ? o[e] + d : d;
       }
       if (ok) store8<T>(dx + row * C + vi * 8, o);
     }
@@ -307,7 +309,8 @@ void fwd_launch(const void* x, const void* w, const void* b, void* y, float* mea
 
 template <typename T, int L, int V>
 void bwd_launch(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx, float* dw,
-                float* db, long rows, int C, int accumulate, float* ws, dfk_drop drop, hipStream_t s) {
+                float* db, long rows, int C, int accumulate, float* ws, dfk_drop drop, const void* addend,
+                hipStream_t s) {
   const int blocks = (int)bwd_blocks(rows, C);
   float* part = ws && (dw || db) ? ws : nullptr;
   // in-launch combine groups: about 48 KB of partials per group's reducer, 8-64 blocks
@@ -315,7 +318,8 @@ void bwd_launch(const void* dy, const void* x, const void* w, const float* mean,
   while (gs > 8 && (long)gs * 8 * C > 49152) gs >>= 1;
   uint32_t* cnt = part ? dfk_ticket_slice(dfk_cdiv(blocks, gs), s) : nullptr;
   hipLaunchKernelGGL((ln_bwd<T, L, V>), dim3(blocks), dim3(256), 2 * C * sizeof(float), s, (const T*)dy,
-                     (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part, drop, cnt, gs);
+                     (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part, drop, cnt, gs,
+                     (const T*)addend);
   if (part && !cnt)
     hipLaunchKernelGGL(slab_colsum, dim3(dfk_cdiv(2 * C, 64), dfk_cdiv(blocks, 256)), dim3(256), 0, s, part, blocks, C,
                        dw, db);
@@ -351,8 +355,9 @@ struct Fwd {
 template <typename T, int L, int V>
 struct Bwd {
   static void run(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
-                  float* dw, float* db, long rows, int C, int accumulate, float* ws, dfk_drop drop, hipStream_t s) {
-    bwd_launch<T, L, V>(dy, x, w, mean, rstd, dx, dw, db, rows, C, accumulate, ws, drop, s);
+                  float* dw, float* db, long rows, int C, int accumulate, float* ws, dfk_drop drop, const void* addend,
+                  hipStream_t s) {
+    bwd_launch<T, L, V>(dy, x, w, mean, rstd, dx, dw, db, rows, C, accumulate, ws, drop, addend, s);
   }
 };
 
@@ -386,13 +391,13 @@ extern "C" int64_t dfk_layernorm_bwd_workspace(int64_t rows, int32_t C) {
 
 extern "C" int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                                  void* dx, float* dw, float* db, int64_t rows, int32_t C, int accumulate, int dtype,
-                                 float* ws, const dfk_drop* drop, hipStream_t s) {
+                                 float* ws, const dfk_drop* drop, const void* addend, hipStream_t s) {
   if (!dy || !x || !w || !mean || !rstd || !dx || C <= 0 || C % 8 || C > 4096 || !drop_ok(drop)) return DFK_EINVAL;
   if (rows <= 0) return 0;
   const dfk_drop d = drop_or_none(drop);
   const bool ok = dtype == DFK_BF16
-                      ? pick<bf16raw, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, ws, d, s)
-                      : pick<float, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, ws, d, s);
+                      ? pick<bf16raw, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, ws, d, addend, s)
+                      : pick<float, Bwd>(C, dy, x, w, mean, rstd, dx, dw, db, (long)rows, (int)C, accumulate, ws, d, addend, s);
   if (!ok) return DFK_EINVAL;
   DFK_CHECK_LAUNCH();
   return 0;

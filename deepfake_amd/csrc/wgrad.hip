@@ -221,8 +221,11 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // 1 = launched, 0 = not applicable (the caller runs the tiled GEMM), < 0 = launch error
 int dfk_wgrad_try(const dfk_gemm_args& g, hipStream_t s) {
-  static const bool off = getenv("DFK_WGRAD") && atoi(getenv("DFK_WGRAD")) == 0;   // A/B runs
-  if (off) return 0;
+  // opt-in (DFK_WGRAD=1): faster than the tiled split-K dW in isolation on the stage-1/2 shapes, slower inside
+  // the replayed step (its one-per-CU persistent workgroups with 100-123 KB of LDS wait for CUs the other branch
+  // streams hold; profiles/gemm/r4o_wgrad_instep.txt)
+  const char* env = getenv("DFK_WGRAD");   // read per call: tests switch it inside one process
+  if (!env || atoi(env) == 0) return 0;
   if (g.dtype != DFK_BF16 || !g.a_kmajor || !g.b_kmajor || !g.c_f32) return 0;
   if (!(g.atomic || g.beta == 1.f)) return 0;   // C += product only (atomics)
   if (g.nz0 != 1 || g.nz1 != 1 || g.a.conv_cg > 0 || g.b.conv_cg > 0) return 0;

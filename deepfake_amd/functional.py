@@ -237,12 +237,11 @@ def linear_group(x, weights, biases=None, skip=False):
 
 
 def _skip_grad_buffer(dskip, like):
-    """The skip path's gradient as a buffer the LN backward may accumulate into in place: autograd hands a
-    Function its grad_output and forgets it once the Function returns, so the residual gradient one Function
-    passes on can carry the next one's sum."""
+    """The skip path's gradient as the LN backward's addend (read only: it is often a view of a grad_output the
+    caller still holds, e.g. the gradient passed to y.backward(dy) at a block's output)."""
     if dskip.dtype == like.dtype and dskip.is_contiguous() and dskip.numel() == like.numel():
-        return dskip.view(like.shape)   # (often a reshape view of the producer's grad_output: same memory)
-    return dskip.to(like.dtype).contiguous().reshape(like.shape).clone()
+        return dskip.view(like.shape)
+    return dskip.to(like.dtype).contiguous().reshape(like.shape)
 
 
 class MlpFn(torch.autograd.Function):
@@ -341,7 +340,7 @@ class LayerNormFn(torch.autograd.Function):
         dw, db = grad_sink(weight), grad_sink(bias)
         if ctx.skip and dskip is not None:   # dx = LN'(dy) + the skip path's gradient, in one pass
             dx = K.layernorm_bwd(dy, x, compute_weight(weight, x.dtype), mean, rstd, dw, db, drop=ctx.drop,
-                                 dx=_skip_grad_buffer(dskip, x), accumulate=True)
+                                 addend=_skip_grad_buffer(dskip, x))
         else:
             dx = K.layernorm_bwd(dy, x, compute_weight(weight, x.dtype), mean, rstd, dw, db, drop=ctx.drop)
         return dx, grad_done(weight, dw), grad_done(bias, db), None, (dy if ctx.has_res else None), None, None

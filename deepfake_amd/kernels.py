@@ -229,8 +229,10 @@ def _ln_bwd_blocks(rows, C):
     return min(2048, -(-rows // (4 * (64 // lanes))))
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False, slab_partials=None, drop=None):
-    """dx (+)= LN backward; dw / db (fp32) += the affine gradients.  slab_partials (default: from 64
+def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False, slab_partials=None, drop=None,
+                  addend=None):
+    """dx (+)= LN backward (+ addend [rows, C] of x's dtype, read: the skip path's gradient summed in the same
+    pass without writing into it); dw / db (fp32) += the affine gradients.  slab_partials (default: from 64
     workgroups up) writes each workgroup's dw/db partial to a slab summed by a column pass instead of adding
     it atomically: hundreds of workgroups adding into the same C addresses serialise on a few L2 channels
     (the 1568 x 512 SwinV2 / wav2vec2 LNs ran 20 us, the 401k x 96 stage-1 LN 116 us)."""
@@ -245,7 +247,7 @@ def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False, slab_
                          dtype=torch.float32)
     L.check(L.lib().dfk_layernorm_bwd(L.ptr(dy), L.ptr(x), L.ptr(w), L.ptr(mean), L.ptr(rstd), L.ptr(dx),
                                       L.ptr(dw), L.ptr(db), rows, C, int(accumulate), L.dt(x), L.ptr(ws),
-                                      L.drop(drop, x.device), L.stream()), "layernorm_bwd")
+                                      L.drop(drop, x.device), L.ptr(addend), L.stream()), "layernorm_bwd")
     return dx
 
 

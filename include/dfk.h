@@ -147,14 +147,16 @@ int dfk_colsum(const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld,
 int dfk_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
                       int64_t rows, int32_t C, float eps, int dtype, const void* residual, const dfk_drop* drop,
                       hipStream_t stream);
-/* dx (=, or += when accumulate) ; dw, db accumulate (+=); drop (may be NULL): the forward's mask applied
- * to dy first (the gradient of drop(LN(x))).  ws: fp32 scratch of
+/* dx = LN'(dy) (+ addend when addend != NULL, else + dx when accumulate); dw, db accumulate (+=); drop (may be
+ * NULL): the forward's mask applied to dy first (the gradient of drop(LN(x))).  addend ([rows][C], dtype): the
+ * gradient of a skip alias of x (the block's residual path), summed in the same pass without writing into the
+ * caller's gradient buffer.  ws: fp32 scratch of
  * dfk_layernorm_bwd_workspace(rows, C) bytes for per-workgroup dw/db partials,
  * column-summed by a second pass; NULL: fp32 atomics per workgroup and channel
  * (same-address contention: slow when many workgroups share few channels). */
 int dfk_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                       void* dx, float* dw, float* db, int64_t rows, int32_t C, int accumulate, int dtype,
-                      float* ws, const dfk_drop* drop, hipStream_t stream);
+                      float* ws, const dfk_drop* drop, const void* addend, hipStream_t stream);
 int64_t dfk_layernorm_bwd_workspace(int64_t rows, int32_t C);
 
 /* Windowed multi-head attention core on token-major buffers (no window

@@ -84,11 +84,13 @@ def test_linear_weight_resident(M, N, Kd):
 @pytest.mark.parametrize("M,N,Kd", [(20000, 288, 96), (16500, 96, 96), (17000, 384, 96), (16400, 96, 384),
                                     (16385, 576, 192), (16384, 192, 768), (20000, 384, 128), (20000, 512, 128),
                                     (16384, 128, 512), (16448, 128, 128), (16400, 384, 768)])
-def test_linear_dw_token_streaming(M, N, Kd):
-    """bf16 weight gradients with >= 16k tokens and a small dW run on the token-streaming kernel (wgrad.hip):
+def test_linear_dw_token_streaming(M, N, Kd, monkeypatch):
+    """bf16 weight gradients with >= 16k tokens and a small dW on the token-streaming kernel (wgrad.hip, opt-in
+    DFK_WGRAD=1):
     every instantiated wave grid, row / column slices (the bias gradient counted once per row), a ragged token
     tail, accumulation into a non-zero dW, and an x that is a column view of a wider buffer (ld > Kd).
     fp32 accumulation of exact bf16 products: checked at 1e-4 of the largest entry."""
+    monkeypatch.setenv("DFK_WGRAD", "1")
     dt = torch.bfloat16
     g = torch.Generator(device=DEV).manual_seed(3)
     xb = torch.randn(M, Kd + 64, device=DEV, generator=g).to(dt)
@@ -104,6 +106,37 @@ def test_linear_dw_token_streaming(M, N, Kd):
     dw2 = torch.zeros(N, Kd, device=DEV)
     K.linear_dw(dy, x, dw2)
     assert rel(dw2, dy.double().t() @ x.double()) < 1e-4
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,Kd", [(1000, 288, 96), (1568, 512, 2048), (1592, 768, 3072), (1592, 2304, 768)])
+def test_inlaunch_combine(dt, M, N, Kd, monkeypatch):
+    """Opt-in in-launch combine (DFK_INLAUNCH_COMBINE=1: arrival tickets, the last split / block group sums the
+    partials): split-K forward / dX / dW GEMMs and the LayerNorm dgamma/dbeta partials equal the default path's
+    results (same split order: bit-identical GEMM outputs)."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(M, Kd, device=DEV, generator=g).to(dt)
+    w = (torch.randn(N, Kd, device=DEV, generator=g) / math.sqrt(Kd)).to(dt)
+    dy = torch.randn(M, N, device=DEV, generator=g).to(dt)
+    ln = torch.nn.LayerNorm(Kd).to(DEV)
+    mean = x.float().mean(1)
+    rstd = (x.float().var(1, unbiased=False) + 1e-5).rsqrt()
+    dyl = torch.randn(M, Kd, device=DEV, generator=g).to(dt)
+
+    def run():
+        dw = torch.zeros(N, Kd, device=DEV)
+        K.linear_dw(dy, x, dw)
+        lw, lb = torch.zeros(Kd, device=DEV), torch.zeros(Kd, device=DEV)
+        dxl = K.layernorm_bwd(dyl, x, ln.weight.to(dt), mean, rstd, lw, lb, slab_partials=True)
+        return K.linear(x, w), K.linear_dx(dy, w), dw, dxl, lw, lb
+    base = run()
+    monkeypatch.setenv("DFK_INLAUNCH_COMBINE", "1")
+    got = run()
+    for i, (a, b) in enumerate(zip(got, base)):
+        if i < 4:
+            assert torch.equal(a, b), i
+        else:   # group sums added atomically: the order of the per-group atomics differs
+            assert rel(a, b) < 1e-5, i
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
