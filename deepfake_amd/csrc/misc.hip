@@ -430,7 +430,9 @@ extern "C" int dfk_sgd_step(float* param, const float* grad, float* momentum_buf
     return DFK_EINVAL;
   if (n <= 0) return 0;
   const long threads = (n + 3) / 4;
-  static const bool nt = !getenv("DFK_SGD_NT") || atoi(getenv("DFK_SGD_NT")) != 0;   // 0: plain stores (A/B runs)
+  // DFK_SGD_NT=1: non-temporal stores (A/B runs; no measurable effect on the step or on the next step's patch
+  // embedding, profiles/step/r4p_conv3d_instep_diagnosis.txt)
+  static const bool nt = getenv("DFK_SGD_NT") && atoi(getenv("DFK_SGD_NT")) != 0;
   auto kfn = nt ? sgd_kernel<true> : sgd_kernel<false>;
   hipLaunchKernelGGL(kfn, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, param, grad, momentum_buf,
                      (bf16raw*)bf16_shadow, (long)n, lr_dev, lr, momentum, weight_decay, first_step, gate);

@@ -4,7 +4,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/r4p; mkdir -p $OUT
 B="python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline"
-for v in "DFK_SGD_NT=1" "DFK_SGD_NT=0" "DFK_WGRAD=1" "DFK_SGD_NT=1"; do
+for v in "DFK_SGD_NT=1" "DFK_SGD_NT=0" "DFK_WGRAD=1" "GPU_MAX_HW_QUEUES=8" "GPU_MAX_HW_QUEUES=6" "DFK_SGD_NT=1"; do
   env $v timeout -k 10 300 $B > $OUT/b.json 2> $OUT/b.err || { tail -20 $OUT/b.err; exit 1; }
   echo "$v: $(python3 -c "import json;d=json.load(open('$OUT/b.json'));print(d['value'], d['ms_per_step'])")"
 done
