@@ -195,10 +195,20 @@ class TrainStep:
             self.first_micro = True
         return outs
 
+    def input_buffers(self):
+        """The replayed graph's input tensors ((video, mel, wave), label), or None before the capture.  A data
+        loader that writes each batch into them in place (and passes them back to __call__) saves the per-step
+        device-to-device copy into the graph's inputs (~0.2 GB at C2, B = 8)."""
+        if self.static is None:
+            return None
+        return tuple(self.static[0]), self.static[1]
+
     def _load_static(self, feature, label):
         for s, x in zip(self.static[0], feature):
-            s.copy_(x, non_blocking=True)
-        self.static[1].copy_(label, non_blocking=True)
+            if x is not s:   # already the graph's input (a loader writing in place): nothing to copy
+                s.copy_(x, non_blocking=True)
+        if label is not self.static[1]:
+            self.static[1].copy_(label, non_blocking=True)
 
     # capture forms, tried in order (multi-GPU): (bucket all-reduces overlapped with backward, BatchNorm
     # running-stat broadcast inside the graph)
