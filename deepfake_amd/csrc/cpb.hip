@@ -39,8 +39,9 @@ __global__ __launch_bounds__(256) void cpb_fwd_kernel(const float* __restrict__ 
 }
 
 // workgroup b sums coordinate rows [b*kRows, b*kRows + kRows); thread t owns hidden units t, t + blockDim.x, ...;
-// partial sums are added with fp32 atomics (a few workgroups per parameter element)
-constexpr int kRows = 16;
+// partial sums are added with fp32 atomics (43 workgroups per parameter element at L = 169: with 16 rows per
+// workgroup the launch ran on 11 CUs)
+constexpr int kRows = 4;
 __global__ __launch_bounds__(512) void cpb_bwd_kernel(const float* __restrict__ c, const float* __restrict__ w1,
                                                       const float* __restrict__ b1, const float* __restrict__ w2,
                                                       const float* __restrict__ out, const float* __restrict__ dout,

@@ -296,7 +296,12 @@ __global__ __launch_bounds__(256) void slab_colsum(const float* __restrict__ par
 long bwd_blocks(long rows, int C) {
   const int nv = C / 8;
   const int L = nv <= 16 ? 16 : (nv <= 32 ? 32 : 64);
-  return std::min<long>(2048, dfk_cdiv(rows, 4L * (64 / L)));
+  // at most 2048 workgroups, 512 from C = 512 up: their [blocks][2C] partial slab, summed by slab_colsum, grows
+  // with C (tools/ln_bench.py, profiles/r4/r4s_ln_bwd_block_cap.txt: [6272, 768] 46 -> 25 us at 512, while the
+  // narrow stage-1/2 rows need the 2048 workgroups: [401408, 96] 65 -> 84 us at 512)
+  static const long env = getenv("DFK_LN_BWD_BLOCKS") ? atol(getenv("DFK_LN_BWD_BLOCKS")) : 0;   // tuning runs
+  const long cap = env > 0 ? env : (C >= 512 ? 512 : 2048);
+  return std::min<long>(cap, dfk_cdiv(rows, 4L * (64 / L)));
 }
 
 template <typename T, int L, int V>

@@ -1,39 +1,39 @@
-"""Micro-benchmark of the LayerNorm kernels at the C2 step's row counts (bf16): time and HBM GB/s."""
+"""LayerNorm forward / backward on the C2 step's shapes (graph-timed per call; backward with the slab
+partials + column pass).  Usage: python tools/ln_bench.py"""
 import os
 import sys
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from deepfake_amd import kernels as K  # noqa: E402
+from gemm_bench import t  # noqa: E402
 
-SHAPES = [(401408, 96), (100352, 192), (100352, 384), (25088, 384), (25088, 768), (6272, 768), (25088, 128),
-          (6272, 512), (1568, 512), (1568, 2048), (1592, 768)]
-
-
-def timed(fn, it=20):
-    fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(it):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / it * 1e3
+SHAPES = [("vst1", 401408, 96), ("vst2", 100352, 192), ("vst3", 25088, 384), ("vst4", 6272, 768),
+          ("mel1", 25088, 128), ("mel3", 1568, 512), ("w2v", 1592, 768), ("mel4", 392, 1024)]
 
 
-for rows, C in SHAPES:
-    x = torch.randn(rows, C, device="cuda").to(torch.bfloat16)
-    w = torch.ones(C, device="cuda", dtype=torch.bfloat16)
-    b = torch.zeros(C, device="cuda", dtype=torch.bfloat16)
-    y, mean, rstd = K.layernorm_fwd(x, w, b)
-    dy = torch.randn_like(x)
-    dw = torch.zeros(C, device="cuda")
-    db = torch.zeros(C, device="cuda")
-    dx = torch.empty_like(x)
-    tf = timed(lambda: K.layernorm_fwd(x, w, b, out=y))
-    tb = timed(lambda: K.layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=dx))
-    nb = rows * C * 2
-    print(f"rows {rows:7d} C {C:5d}  fwd {tf:7.1f} us {2 * nb / tf / 1e3:6.0f} GB/s | bwd {tb:7.1f} us "
-          f"{3 * nb / tb / 1e3:6.0f} GB/s", flush=True)
+def main():
+    tot = [0.0, 0.0]
+    for name, rows, C in SHAPES:
+        x = torch.randn(rows, C, device="cuda").to(torch.bfloat16)
+        w = torch.ones(C, device="cuda").to(torch.bfloat16)
+        b = torch.zeros(C, device="cuda").to(torch.bfloat16)
+        dy = torch.randn(rows, C, device="cuda").to(torch.bfloat16)
+        y, mean, rstd = K.layernorm_fwd(x, w, b)
+        dw = torch.zeros(C, device="cuda")
+        db = torch.zeros(C, device="cuda")
+        dx = torch.empty_like(x)
+        f = t(lambda: K.layernorm_fwd(x, w, b))
+        bw = t(lambda: K.layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=dx))
+        tot[0] += f
+        tot[1] += bw
+        mb = rows * C * 2 * 3 / 1e6
+        print(f"{name:5s} rows {rows:6d} C {C:4d}  fwd {f*1e6:6.1f} us  bwd {bw*1e6:6.1f} us "
+              f"({mb / (bw * 1e6) * 1e3:6.0f} GB/s of dy + x + dx)", flush=True)
+    print(f"totals us: fwd {tot[0]*1e6:.1f} bwd {tot[1]*1e6:.1f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
