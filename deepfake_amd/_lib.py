@@ -115,7 +115,8 @@ SIGNATURES = {
     "dfk_cosine_qk_bwd": [_VP, _VP, _VP, _VP, _F, _VP, _I64, C.c_int, C.c_int, C.c_int, _VP],
     "dfk_cpb_bias_fwd": [_VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],
     "dfk_cpb_bias_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],
-    "dfk_w2v_conv0_fwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP],
+    "dfk_w2v_conv0_fwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _VP],
+    "dfk_w2v_conv0_fwd_workspace": [_I64, _I64],
     "dfk_w2v_conv0_bwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _I64, _VP, _VP, _VP, _VP],
     "dfk_w2v_conv0_bwd_workspace": [_I64, _I64],
     "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP, _VP],
@@ -145,7 +146,7 @@ SIGNATURES = {
 }
 
 _lib = None
-RESTYPES = {"dfk_mel_workspace": _I64, "dfk_w2v_conv0_bwd_workspace": _I64, "dfk_layernorm_bwd_workspace": _I64, "dfk_wattn_bwd_workspace": _I64, "dfk_wattn_table_workspace": _I64, "dfk_gemm_workspace": _I64}
+RESTYPES = {"dfk_mel_workspace": _I64, "dfk_w2v_conv0_bwd_workspace": _I64, "dfk_w2v_conv0_fwd_workspace": _I64, "dfk_layernorm_bwd_workspace": _I64, "dfk_wattn_bwd_workspace": _I64, "dfk_wattn_table_workspace": _I64, "dfk_gemm_workspace": _I64}
 
 
 def lib():

@@ -34,9 +34,9 @@ __device__ __forceinline__ float conv_at(const float* xs, const float* ws, int t
   return y;
 }
 
-// pass 1: per (b, c) sum and sum of squares of y over time (fp32 atomics)
+// pass 1: per (b, time block, c) partial sum and sum of squares of y -> the partial slab [b][block][c][2]
 __global__ __launch_bounds__(256) void conv0_stats(const float* __restrict__ x, const float* __restrict__ w, long S,
-                                                   int T0, float* __restrict__ stats) {
+                                                   int T0, float* __restrict__ part) {
   __shared__ float xs[TB * KS + KW];
   __shared__ float ws[CH * KW];
   const int b = blockIdx.y, t0 = blockIdx.x * TB;
@@ -49,9 +49,30 @@ __global__ __launch_bounds__(256) void conv0_stats(const float* __restrict__ x, 
       s += y;
       q += y * y;
     }
-    atomicAdd(stats + ((long)b * CH + c) * 2, s);
-    atomicAdd(stats + ((long)b * CH + c) * 2 + 1, q);
+    float* dst = part + (((long)b * gridDim.x + blockIdx.x) * CH + c) * 2;
+    dst[0] = s;
+    dst[1] = q;
   }
+}
+
+// pass 1b: stats[b][c][2] = sum over the time blocks of the partials, in a fixed order (4 interleaved row phases,
+// then (p0 + p1) + (p2 + p3)): the forward's GroupNorm statistics, and so the loss, are bitwise reproducible
+__global__ __launch_bounds__(256) void conv0_stats_sum(const float* __restrict__ part, int nblk,
+                                                       float* __restrict__ stats) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.y, lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;   // column of the [CH][2] row
+  const float* src = part + (long)b * nblk * CH * 2 + j;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  int r = ph;
+  for (; r + 12 < nblk; r += 16) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += src[(long)(r + 4 * u) * CH * 2];
+  }
+  for (; r < nblk; r += 4) a[0] += src[(long)r * CH * 2];
+  red[ph][lane] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (ph == 0) stats[(long)b * CH * 2 + j] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 // pass 2: out = gelu(gn(y)); one thread per (t, channel pair) -> coalesced channels-last stores
@@ -205,13 +226,21 @@ extern "C" int64_t dfk_w2v_conv0_bwd_workspace(int64_t B, int64_t S) {
   return (int64_t)4 * (B * CH * 2 + B * conv0_dw_blocks(B, T0) * (int64_t)(CH * KW));
 }
 
+extern "C" int64_t dfk_w2v_conv0_fwd_workspace(int64_t B, int64_t S) {
+  if (B <= 0 || S < KW) return 0;
+  const int T0 = (int)((S - KW) / KS + 1);
+  return (int64_t)4 * B * dfk_cdiv(T0, TB) * CH * 2;
+}
+
 extern "C" int dfk_w2v_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
-                                 const float* beta, float eps, float* stats, void* out, int dtype, hipStream_t s) {
-  if (!wave || !w || !gamma || !beta || !stats || !out || S < KW) return DFK_EINVAL;
+                                 const float* beta, float eps, float* stats, void* out, int dtype, float* ws,
+                                 hipStream_t s) {
+  if (!wave || !w || !gamma || !beta || !stats || !out || !ws || S < KW) return DFK_EINVAL;
   const int T0 = (int)((S - KW) / KS + 1);
   const dim3 grid(dfk_cdiv(T0, TB), (unsigned)B);
-  (void)hipMemsetAsync(stats, 0, sizeof(float) * B * CH * 2, s);
-  hipLaunchKernelGGL(conv0_stats, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats);
+  static_assert((CH * 2) % 64 == 0, "stats columns per workgroup");
+  hipLaunchKernelGGL(conv0_stats, grid, dim3(256), 0, s, wave, w, (long)S, T0, ws);
+  hipLaunchKernelGGL(conv0_stats_sum, dim3(CH * 2 / 64, (unsigned)B), dim3(256), 0, s, ws, (int)grid.x, stats);
   if (dtype == DFK_BF16)
     hipLaunchKernelGGL(conv0_apply<bf16raw>, grid, dim3(256), 0, s, wave, w, (long)S, T0, stats, gamma, beta, eps,
                        (bf16raw*)out);

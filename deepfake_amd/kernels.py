@@ -428,8 +428,9 @@ def w2v_conv0_fwd(wave, w, gamma, beta, eps, dtype):
     T0 = (S - 10) // 5 + 1
     out = torch.empty(B, T0, 512, device=wave.device, dtype=dtype)
     stats = torch.empty(B, 512, 2, device=wave.device, dtype=torch.float32)
+    ws = torch.empty(max(L.lib().dfk_w2v_conv0_fwd_workspace(B, S) // 4, 1), device=wave.device, dtype=torch.float32)
     L.check(L.lib().dfk_w2v_conv0_fwd(L.ptr(wave), B, S, L.ptr(w), L.ptr(gamma), L.ptr(beta), float(eps),
-                                      L.ptr(stats), L.ptr(out), L.dt(out), L.stream()), "w2v_conv0_fwd")
+                                      L.ptr(stats), L.ptr(out), L.dt(out), L.ptr(ws), L.stream()), "w2v_conv0_fwd")
     return out, stats
 
 

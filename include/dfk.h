@@ -284,7 +284,10 @@ int dfk_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, hipStr
  * [512] fp32; stats [B,512,2] fp32 (sum, sumsq of the conv output) saved for
  * the backward.  The conv output is recomputed, never stored. */
 int dfk_w2v_conv0_fwd(const float* wave, int64_t B, int64_t S, const float* w, const float* gamma,
-                      const float* beta, float eps, float* stats, void* out, int dtype, hipStream_t stream);
+                      const float* beta, float eps, float* stats, void* out, int dtype, float* ws, hipStream_t stream);
+/* ws: fp32 scratch of dfk_w2v_conv0_fwd_workspace(B, S) bytes for the per-time-block GroupNorm partial sums,
+ * summed into stats in a fixed order (the forward is bitwise reproducible: no atomics). */
+int64_t dfk_w2v_conv0_fwd_workspace(int64_t B, int64_t S);
 /* backward: dw [512,10], dgamma, dbeta fp32 (+=); scratch: fp32 buffer of scratch_bytes >=
  * dfk_w2v_conv0_bwd_workspace(B, S) bytes (the [B,512,2] GroupNorm reductions, then per-workgroup dw partials
  * summed without atomics); a smaller buffer returns DFK_EINVAL. */
