@@ -90,7 +90,7 @@ def time_kernel(fn, iters):
 
 
 ROOFLINE_KERNEL = "wattn_fwd4_kernel<32, false, 2>"
-ROOFLINE_PMC = os.path.join(HERE, "profiles", "r3o_wattn_fwd_pmc.json")
+ROOFLINE_PMC = os.path.join(HERE, "profiles", "r4", "r4z_wattn_fwd_pmc.json")   # tools/gpu_round4.sh r4z
 
 
 def stage1_geometry(cfg):
@@ -146,7 +146,7 @@ def pmc_traffic():
 
 
 CONV3D_KERNEL = "pe_fwd_kernel<6>"
-CONV3D_INSTEP = os.path.join(HERE, "profiles", "r3o_conv3d_instep.json")
+CONV3D_INSTEP = os.path.join(HERE, "profiles", "r4", "r4z_conv3d_instep.json")   # tools/gpu_round4.sh r4z
 
 
 def conv3d_in_step():
