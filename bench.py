@@ -251,6 +251,35 @@ def gemm_roofline(cfg, B, iters, fp8=False):
             "bytes_per_launch": (M * Kd + 2 * M * N + N * Kd) * 2, "avg_launch_ms": round(t * 1e3, 4)}
 
 
+DW_KERNEL = "gemm_dma_kernel<64, 2, 2, true, true, 2, true, false>"
+
+
+def dw_roofline(cfg, B, iters):
+    """The step's largest weight-gradient launch: the video trunk's stage-1 Mlp.fc1 dW with its fused bias gradient
+    (src/utils.py:254-256 backward): dW[4C, C] += dy[tokens, 4C]^T x[tokens, C], db[4C] += colsum(dy), tokens =
+    B * (T/2) * (H/4) * (W/4) (401k at C2), split over the tokens with fp32 atomics (kernels.linear_dw).  K = C is
+    small, so the launch is HBM-bound: algorithmic bytes = tokens * 5C * 2 (dy and x read once, bf16) + the fp32
+    dW / db read-modify-write."""
+    from deepfake_amd import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(10)
+    C = cfg["vst"]["embed_dim"]
+    M = B * (cfg["T"] // 2) * (cfg["H"] // 4) * (cfg["W"] // 4)
+    x = torch.randn(M, C, device="cuda", generator=g).to(torch.bfloat16)
+    dy = torch.randn(M, 4 * C, device="cuda", generator=g).to(torch.bfloat16)
+    dw = torch.zeros(4 * C, C, device="cuda")
+    db = torch.zeros(4 * C, device="cuda")
+
+    def run():
+        K.linear_dw(dy, x, dw, db=db)
+    t = time_kernel(run, iters)
+    nbytes = M * 5 * C * 2 + (4 * C * C + 4 * C) * 8
+    achieved = nbytes / t / 1e9
+    return {"kernel": DW_KERNEL + f" (stage-1 Mlp.fc1 weight + bias gradient, [{M},{4 * C}]^T x [{M},{C}], token split, "
+            "fp32 atomics)", "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 4), "bytes_per_launch": nbytes,
+            "flops_per_launch": 2.0 * M * 4 * C * C, "avg_launch_ms": round(t * 1e3, 4)}
+
+
 def _cpu_train_rate(cfg_name, B, steps):
     """Median seconds per fp32 CPU train step (fwd + BCE + bwd + SGD, train-mode BatchNorm) of the oracle."""
     from oracle import fusion as OF
@@ -383,6 +412,7 @@ def main():
     roof = roofline(cfg, a.batch, dt, a.roofline_iters, pmc=c2) if rank == 0 else None
     roof_conv = conv3d_roofline(cfg, a.batch, a.roofline_iters, instep=c2) if rank == 0 else None
     roof_gemm = gemm_roofline(cfg, a.batch, a.roofline_iters, fp8=a.dtype == "fp8") if rank == 0 else None
+    roof_dw = dw_roofline(cfg, a.batch, a.roofline_iters) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
@@ -402,7 +432,8 @@ def main():
                        "branch_streams": 3,
                        "regularisers": not a.deterministic, "loss": round(lossv, 5)},
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2) if train_gflop else None,
-            "roofline": roof, "roofline_conv3d": roof_conv, "roofline_gemm": roof_gemm, "cpu_baseline": cpu,
+            "roofline": roof, "roofline_conv3d": roof_conv, "roofline_gemm": roof_gemm, "roofline_dw": roof_dw,
+            "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
