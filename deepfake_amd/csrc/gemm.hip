@@ -835,6 +835,14 @@ void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int eve
     return;
   }
   const int st = dma_stages(wt);
+  if (wt == 33) {   // 128 x 64 (8 waves of 32 x 32)
+    dispatch_dma_s<32, 4, 2, 2>(g, grid, kchunk, evec, sk, s);
+    return;
+  }
+  if (wt == 34) {   // 64 x 128
+    dispatch_dma_s<32, 2, 4, 2>(g, grid, kchunk, evec, sk, s);
+    return;
+  }
   if (wt == 128) {
     if (st == 3) dispatch_dma_s<64, 4, 2, 3>(g, grid, kchunk, evec, sk, s);
     else dispatch_dma_s<64, 4, 2, 2>(g, grid, kchunk, evec, sk, s);
@@ -930,16 +938,26 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   int wt = pick_wt(g);
   const bool dma = sizeof(T) == 2 && dma_ok(g);
   const bool conv = g.a.conv_cg > 0 || g.b.conv_cg > 0;
-  if (dma && wt == 64 && !conv) {   // 256x128 tiles (8 waves) when the grid still covers the chip (tuning knob for now)
+  // vector path also needs the contiguous extents to be whole vectors (else tails load element-wise)
+  const bool vec = view_vec(g.a, VEC) && view_vec(g.b, VEC) && (g.a_kmajor ? g.M : g.K) % VEC == 0 &&
+                   (g.b_kmajor ? g.N : g.K) % VEC == 0;
+  if (dma && vec && wt == 64 && !conv) {   // 256x128 tiles (8 waves) when the grid still covers the chip (tuning knob for now)
     static const long t256 = getenv("DFK_GEMM_T256") ? atol(getenv("DFK_GEMM_T256")) : (1L << 40);
     const long tiles256 = (long)dfk_cdiv(g.N, 128) * dfk_cdiv(g.M, 256) * g.nz0 * g.nz1 * gg.splitk;
     if (tiles256 >= t256) wt = 128;
   }
-  dim3 grid(dfk_cdiv(g.N, wt == 128 ? 128 : 2 * wt), dfk_cdiv(g.M, wt == 128 ? 256 : 2 * wt), g.nz0 * g.nz1 * gg.splitk);
+  if (dma && vec && wt == 32 && !conv) {
+    // small grids, forward and dX: 8-wave 128x64 / 64x128 workgroups of 32x32 waves, the longer side along the
+    // larger of M / N (each staged tile feeds twice the MFMA work of a 4-wave 64x64 one; r4u: C2 247.1 -> 250.6
+    // clips/s, vst4.fc1 dX 69 -> 49 us); the dW GEMMs (k-major A) keep 64x64 (their fp32 epilogue lost there)
+    static const int t32x = getenv("DFK_GEMM_T32X") ? atoi(getenv("DFK_GEMM_T32X")) : -1;   // A/B: 0 / 1 / 2
+    if (t32x == 1 || (t32x < 0 && !g.a_kmajor && g.M >= g.N)) wt = 33;
+    else if (t32x == 2 || (t32x < 0 && !g.a_kmajor)) wt = 34;
+  }
+  const int bm = wt == 128 ? 256 : (wt == 33 ? 128 : (wt == 34 ? 64 : 2 * wt));
+  const int bn = wt == 128 ? 128 : (wt == 33 ? 64 : (wt == 34 ? 128 : 2 * wt));
+  dim3 grid(dfk_cdiv(g.N, bn), dfk_cdiv(g.M, bm), g.nz0 * g.nz1 * gg.splitk);
   if (grid.y > 65535 || grid.z > 65535) return DFK_EINVAL;
-  // vector path also needs the contiguous extents to be whole vectors (else tails load element-wise)
-  const bool vec = view_vec(g.a, VEC) && view_vec(g.b, VEC) && (g.a_kmajor ? g.M : g.K) % VEC == 0 &&
-                   (g.b_kmajor ? g.N : g.K) % VEC == 0;
   // epilogue 16-B path: 8-element groups of C / residual / aux / bias rows stay 16-B aligned
   const bool evec = !g.c_f32 && aligned16(g.c) && g.ldc % 8 == 0 && g.cbs0 % 8 == 0 && g.cbs1 % 8 == 0 &&
                     (!g.bias || (aligned16(g.bias) && g.bias_bs1 % 8 == 0)) &&

@@ -32,3 +32,8 @@ if [ "$4" == "pe-pmc" ]; then
   python3 tools/pe_pmc.py $(find $OUT/pe_f -name run_counter_collection.csv) $(find $OUT/pe_w -name run_counter_collection.csv) > $OUT/${TAG}_conv3d_pmc.txt
   cat $OUT/${TAG}_conv3d_pmc.txt
 fi
+if [ "$5" == "c4" ]; then
+  timeout -k 10 400 python3 -u bench.py --config c4 --dtype fp8 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/${TAG}_c4_fp8_bench_line.json 2> $OUT/c4_fp8.err || { tail -20 $OUT/c4_fp8.err; exit 1; }
+  timeout -k 10 400 python3 -u bench.py --config c4 --dtype bf16 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/${TAG}_c4_bf16_bench_line.json 2> $OUT/c4_bf16.err || { tail -20 $OUT/c4_bf16.err; exit 1; }
+  cut -c1-160 $OUT/${TAG}_c4_fp8_bench_line.json $OUT/${TAG}_c4_bf16_bench_line.json
+fi
