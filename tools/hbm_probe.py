@@ -21,3 +21,7 @@ c = torch.empty(n // 4, dtype=torch.bfloat16, device="cuda")
 print(f"fill  {n * 2 / t(lambda: a.fill_(1.0)) / 1e12:.2f} TB/s (write only, {n * 2 / 1e6:.0f} MB)")
 print(f"copy  {n * 4 / t(lambda: a.copy_(b)) / 1e12:.2f} TB/s (read + write)")
 print(f"small-read big-write {n * 2.5 / t(lambda: a.view(-1, 4).copy_(c.view(-1, 1).expand(-1, 4))) / 1e12:.2f} TB/s")
+# write-heavy mixes of the stage-1 GELU Linear: read 77 MB, write 2 x 308 MB
+x = torch.empty(401408 * 96, dtype=torch.bfloat16, device="cuda")
+print(f"fill x2 {2 * n * 2 / t(lambda: (a.fill_(1.0), b.fill_(2.0))) / 1e12:.2f} TB/s (two write-only streams)")
+print(f"read 77 MB + write 2 x 308 MB (expand) {(n * 4 + x.numel() * 2) / t(lambda: (a.view(-1, 4).copy_(x.view(-1, 1).expand(-1, 4)), b.view(-1, 4).copy_(x.view(-1, 1).expand(-1, 4)))) / 1e12:.2f} TB/s")
