@@ -26,6 +26,11 @@ template <typename T> __device__ __forceinline__ void stf(T* p, float v);
 template <> __device__ __forceinline__ void stf<float>(float* p, float v) { *p = v; }
 template <> __device__ __forceinline__ void stf<bf16raw>(bf16raw* p, float v) { *p = f2bf(v); }
 
+// DFK_ST_NT: bf16 st8 stores carry the non-temporal hint (streaming outputs; experiment builds)
+#ifndef DFK_ST_NT
+#define DFK_ST_NT 0
+#endif
+
 // 8 consecutive elements <-> fp32 (16-B aligned: one bf16 vector / two f32 vectors)
 template <typename T>
 __device__ __forceinline__ void ld8(const T* p, float* v) {
@@ -48,7 +53,12 @@ __device__ __forceinline__ void st8(T* p, const float* v) {
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+#if DFK_ST_NT
+    typedef unsigned int u32x4nt __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(u32x4nt{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4nt*>(p));
+#else
     *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+#endif
   } else {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);

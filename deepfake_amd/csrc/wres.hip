@@ -23,6 +23,11 @@
 
 namespace {
 
+// cache policy of the output stores (buffer-store aux bits; 2 = non-temporal)
+#ifndef DFK_WRES_NT
+#define DFK_WRES_NT 0
+#endif
+
 constexpr int WRES_LIMIT = 49152;      // W slice elements (96 KiB bf16) -> one 8-wave workgroup per CU
 constexpr int NT = 512;                // 8 waves x 16 token rows = 128-row tiles
 
@@ -85,12 +90,13 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   const DropCtx dc = drop_ctx(g.drop);   // dropout / DropPath of the output (mode 0: none)
   const bf16raw* wbase = w_lds + (cg * NBW * 16 + mrow) * WS + kq;
   const int c0 = n0 + cg * NBW * 16;                    // first channel of this wave's columns
-  // absent bias / residual: read C itself (always valid memory) and clear the bits (C may hold NaN patterns,
-  // so no multiply-by-zero), so every epilogue load is unconditional (channels clamped into range)
-  const bf16raw* bsrc = bias ? bias : C;
+  // absent bias / residual: read the weight's first N elements instead (always valid; row stride 0, so
+  // the loads stay in the L2 and add no HBM traffic — reading C here cost a full output's worth of reads) and
+  // clear the bits (no multiply-by-zero: the data may hold NaN patterns), so every epilogue load is unconditional
+  const bf16raw* bsrc = bias ? bias : W;
   const uint32_t bmask = bias ? 0xffffffffu : 0u;
-  const bf16raw* rsrc = res ? res : C;
-  const long rld = res ? g.ldr : g.ldc;
+  const bf16raw* rsrc = res ? res : W;
+  const long rld = res ? g.ldr : 0;
   const uint32_t rmask = res ? 0xffffffffu : 0u;
   // buffer descriptors of the outputs: exactly the M rows (bounds-checked stores)
   auto rsrc_of = [&](void* p, long ld) {
@@ -179,7 +185,7 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
         const u32x4 u = *reinterpret_cast<const u32x4*>(stg + r * SS + ch);
         const long e = (mt0 + r) * ld + c0 + ch;            // element offset
         const uint32_t off = (c0 + ch < g.N && e < 0x7fffffffL) ? (uint32_t)(e * 2) : 0xfffffff0u;
-        __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, DFK_WRES_NT);
       }
       lds_sync();                                         // reads done before the tile is rewritten
     };
@@ -245,14 +251,28 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   uint4 a0[KC], a1[KC];
   load_a(min(t, ntiles - 1), a0);
   if constexpr (DEPTH == 2) load_a(min(t + stride, ntiles - 1), a1);
+  // epilogue operands one tile ahead (EPF): tile tt's were requested during the previous tile, so their HBM
+  // latency (residual / gelu input rows) hides behind that tile instead of stalling this one's epilogue; the
+  // 9-block-wide and K >= 288 variants have no registers for a second set (they spilled) and load in the tile
+  constexpr bool EPF = NBW == 6 && KC <= 8;
+  uint2 bb[NBW], rr[NBW], ax[NAX];
+  if constexpr (EPF) load_epi(t, bb, rr, ax);
   auto step = [&](uint4 (&buf)[KC], int tt) {
     uint4 cur[KC];
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) cur[kc] = buf[kc];
-    uint2 bb[NBW], rr[NBW], ax[NAX];
-    load_epi(tt, bb, rr, ax);
+    uint2 cb[NBW], cr[NBW], cx[NAX];
+    if constexpr (EPF) {
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) { cb[nb] = bb[nb]; cr[nb] = rr[nb]; }
+#pragma unroll
+      for (int nb = 0; nb < NAX; ++nb) cx[nb] = ax[nb];
+      load_epi(tt + stride, bb, rr, ax);
+    } else {
+      load_epi(tt, cb, cr, cx);
+    }
     load_a(min(tt + DEPTH * stride, ntiles - 1), buf);
-    process(tt, cur, bb, rr, ax);
+    process(tt, cur, cb, cr, cx);
   };
   for (; t < ntiles; t += DEPTH * stride) {
     step(a0, t);
