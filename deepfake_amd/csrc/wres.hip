@@ -35,16 +35,21 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <int KC, int NBW, int NSPLIT>
-constexpr int wres_lds() { return (NBW * 16 * NSPLIT * (KC * 32 + 8) + 8 * 16 * (NBW * 16 + 8)) * 2; }
+constexpr int wres_lds() { return (NBW * 16 * NSPLIT * (KC * 32 + 8) + 8 * 16 * (NBW * 16 + 8)) * 2 + NBW * 16 * NSPLIT * 4; }
 
-// one 8-wave workgroup per CU (2 waves per SIMD, <= 256 VGPRs)
+// Workgroups per CU: two (4 waves per SIMD, <= 128 VGPRs) where the W slice, the staging tiles and the bias fit
+// twice in the LDS (K <= 128 at 6 column blocks) — the launches are latency-bound, so twice the waves in flight
+// is twice the bytes in flight — otherwise one (2 waves per SIMD, <= 256 VGPRs).
+#ifndef DFK_WRES_TWO
+#define DFK_WRES_TWO 0
+#endif
 template <int KC, int NBW, int NSPLIT>
-constexpr bool wres_two_per_cu() { return false; }   // the 128-VGPR variant spilled (the epilogue's loads in flight)
+constexpr bool wres_two_per_cu() { return DFK_WRES_TWO && NBW == 6 && KC <= 4; }
 
-// ACT: 0 plain, 1 GELU (pre-activation -> aux), 2 times gelu'(aux) — a template so the epilogue has no
-// data-dependent branches around its loads (a branch around a load makes the compiler wait vmcnt(0) there,
-// and vmcnt also counts the previous tile's stores)
-template <int KC, int NBW, int NSPLIT, int ACT>
+// ACT: 0 plain, 1 GELU (pre-activation -> aux), 2 times gelu'(aux); RES: residual add.  Template parameters so
+// the epilogue has no data-dependent branches around its loads (a branch around a load makes the compiler wait
+// vmcnt(0) there, and vmcnt also counts the previous tile's stores) and loads nothing it does not use
+template <int KC, int NBW, int NSPLIT, int ACT, bool RES>
 __global__ __launch_bounds__(512, (wres_two_per_cu<KC, NBW, NSPLIT>() ? 4 : 2))
 void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   // slice of BN = NSPLIT*NBW*16 output channels; the 8 waves form (8/NSPLIT) row groups x NSPLIT column
@@ -53,6 +58,7 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   constexpr int ROWS_T = 16 * (8 / NSPLIT);
   constexpr int SS = NBW * 16 + 8;                                 // output staging row stride
   __shared__ __attribute__((aligned(16))) bf16raw w_lds[BN * WS + 8 * 16 * SS];
+  __shared__ __attribute__((aligned(16))) float b_lds[BN];   // the slice's bias (0 without one), fp32
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   bf16raw* stg = w_lds + BN * WS + wave * 16 * SS;
   const int rg = wave / NSPLIT, cg = wave % NSPLIT;
@@ -79,10 +85,11 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
       for (int i = 0; i < 8; ++i) w_lds[(jc + i) * WS + k] = e[i];
     }
   }
+  const bf16raw* bias = reinterpret_cast<const bf16raw*>(g.bias);
+  for (int j = tid; j < BN; j += NT) b_lds[j] = bias && n0 + j < g.N ? bf2f(bias[n0 + j]) : 0.f;
   __syncthreads();
 
   const bf16raw* A = reinterpret_cast<const bf16raw*>(g.a.ptr);
-  const bf16raw* bias = reinterpret_cast<const bf16raw*>(g.bias);
   const bf16raw* res = reinterpret_cast<const bf16raw*>(g.residual);
   bf16raw* aux = reinterpret_cast<bf16raw*>(g.aux);
   bf16raw* C = reinterpret_cast<bf16raw*>(g.c);
@@ -90,14 +97,6 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   const DropCtx dc = drop_ctx(g.drop);   // dropout / DropPath of the output (mode 0: none)
   const bf16raw* wbase = w_lds + (cg * NBW * 16 + mrow) * WS + kq;
   const int c0 = n0 + cg * NBW * 16;                    // first channel of this wave's columns
-  // absent bias / residual: read the weight's first N elements instead (always valid; row stride 0, so
-  // the loads stay in the L2 and add no HBM traffic — reading C here cost a full output's worth of reads) and
-  // clear the bits (no multiply-by-zero: the data may hold NaN patterns), so every epilogue load is unconditional
-  const bf16raw* bsrc = bias ? bias : W;
-  const uint32_t bmask = bias ? 0xffffffffu : 0u;
-  const bf16raw* rsrc = res ? res : W;
-  const long rld = res ? g.ldr : 0;
-  const uint32_t rmask = res ? 0xffffffffu : 0u;
   // buffer descriptors of the outputs: exactly the M rows (bounds-checked stores)
   auto rsrc_of = [&](void* p, long ld) {
     const long bytes = (long)g.M * ld * 2;
@@ -110,32 +109,29 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   auto load_a = [&](int t, uint4 (&fr)[KC]) {
     const long m = (long)t * ROWS_T + rg * 16 + mrow;
     const bool ok = m < g.M;
+    // rows past M read row 0 and are NOT zeroed: output row m depends on A row m alone and the stores drop rows
+    // >= M.  (Zeroing them made the compiler place the mask — and an s_waitcnt vmcnt(0) on this very prefetch,
+    // and every store before it — at the end of the previous tile, so no load or store was ever in flight
+    // across a tile boundary.)
     const bf16raw* p = A + (ok ? m : 0) * g.a.ld + kq;
 #pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      uint4 v = *reinterpret_cast<const uint4*>(p + kc * 32);
-      if (!ok) v = make_uint4(0, 0, 0, 0);
-      fr[kc] = v;
-    }
+    for (int kc = 0; kc < KC; ++kc) fr[kc] = *reinterpret_cast<const uint4*>(p + kc * 32);
   };
 
-  constexpr int NAX = ACT == 2 ? NBW : 1;
-  // the tile's epilogue operands (bias, residual, gelu input): requested BEFORE the next tile's A prefetch,
-  // so the epilogue's waits on them (vmcnt counts in issue order) leave that prefetch in flight
-  auto load_epi = [&](int t, uint2 (&bb)[NBW], uint2 (&rr)[NBW], uint2 (&ax)[NAX]) {
+  constexpr int NAX = ACT == 2 ? NBW : 1, NRR = RES ? NBW : 1;
+  // the tile's per-token epilogue operands (residual, gelu input rows; the bias is in LDS)
+  auto load_epi = [&](int t, uint2 (&rr)[NRR], uint2 (&ax)[NAX]) {
     const long m = (long)t * ROWS_T + rg * 16 + mrow;
     const long mc = m < g.M ? m : g.M - 1;               // clamped row (the store mask drops the tail)
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
       const int n = min(c0 + nb * 16 + nq, g.N - 4);
-      bb[nb] = *reinterpret_cast<const uint2*>(bsrc + n);
-      rr[nb] = *reinterpret_cast<const uint2*>(rsrc + mc * rld + n);
+      if constexpr (RES) rr[nb] = *reinterpret_cast<const uint2*>(res + mc * g.ldr + n);
       if constexpr (ACT == 2) ax[nb] = *reinterpret_cast<const uint2*>(aux + mc * g.ldaux + n);
     }
   };
 
-  auto process = [&](int t, const uint4 (&a_cur)[KC], const uint2 (&bb)[NBW], const uint2 (&rr)[NBW],
-                     const uint2 (&ax)[NAX]) {
+  auto process = [&](int t, const uint4 (&a_cur)[KC], const uint2 (&rr)[NRR], const uint2 (&ax)[NAX]) {
     const long m = (long)t * ROWS_T + rg * 16 + mrow;
 
     f32x4 acc[NBW];
@@ -163,9 +159,8 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
     // a per-wave LDS tile so that global stores are whole 16-B chunks of token rows (8-B stores scattered
     // over 16 rows per instruction ran the write-heavy launches at 2.2-2.8 TB/s)
     auto bias4 = [&](int nb, float (&v)[4]) {
-      const uint2 b = make_uint2(bb[nb].x & bmask, bb[nb].y & bmask);
-      v[0] = acc[nb][0] + __uint_as_float(b.x << 16); v[1] = acc[nb][1] + __uint_as_float(b.x & 0xffff0000u);
-      v[2] = acc[nb][2] + __uint_as_float(b.y << 16); v[3] = acc[nb][3] + __uint_as_float(b.y & 0xffff0000u);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(b_lds + cg * NBW * 16 + nb * 16 + nq);
+      v[0] = acc[nb][0] + b[0]; v[1] = acc[nb][1] + b[1]; v[2] = acc[nb][2] + b[2]; v[3] = acc[nb][3] + b[3];
     };
     const long mt0 = (long)t * ROWS_T + rg * 16;          // first token of this wave's tile
     // LDS-only wave syncs: a release fence would also wait vmcnt(0), i.e. for the next tile's A prefetch
@@ -233,52 +228,55 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] *= drop_mul(dc, m, n + e);
         }
-        const uint2 r = make_uint2(rr[nb].x & rmask, rr[nb].y & rmask);
-        v[0] += __uint_as_float(r.x << 16); v[1] += __uint_as_float(r.x & 0xffff0000u);
-        v[2] += __uint_as_float(r.y << 16); v[3] += __uint_as_float(r.y & 0xffff0000u);
+        if constexpr (RES) {
+          const uint2 r = rr[nb];
+          v[0] += __uint_as_float(r.x << 16); v[1] += __uint_as_float(r.x & 0xffff0000u);
+          v[2] += __uint_as_float(r.y << 16); v[3] += __uint_as_float(r.y & 0xffff0000u);
+        }
         put(nb, v, C, g.ldc);
       }
       flush(rC, g.ldc);
     }
   };
 
-  // A fragments of the next DEPTH tiles are in flight while a tile computes (a register ring: 2 deep for the
-  // K = 96 Linears of Swin stage 1, whose tiles are shortest; deeper rings spilled).  The loop body handles
-  // DEPTH tiles with no exit in between: a tile index past the end computes on clamped loads and its stores
-  // fall outside the output descriptor (rows >= M), so no branch surrounds a load or a store.
-  constexpr int DEPTH = (KC == 3 && NBW == 6) ? 2 : 1;
+  // Software pipeline.  RING2 (the narrow-K variants with registers to spare): two register sets of A fragments
+  // and epilogue operands, the loop unrolled by two tiles; tile tt + 2 stride is requested into the set tile tt
+  // has just consumed, so each load has a whole tile in flight and no register is ever copied (a copy of a
+  // loaded register waits for the load — an earlier form copied the freshly issued prefetch and waited vmcnt(0),
+  // i.e. for it and every store, once per tile).  Otherwise one set: the next tile's A is requested before this
+  // tile computes (copied first), its epilogue operands at its start.  A tile index past the end computes on
+  // clamped loads and its stores fall outside the output descriptor (rows >= M): no branch surrounds a load or
+  // a store.
+  constexpr bool RING2 = NBW == 6 && KC <= 8 && !wres_two_per_cu<KC, NBW, NSPLIT>();
   int t = blockIdx.x / nslices;
-  uint4 a0[KC], a1[KC];
-  load_a(min(t, ntiles - 1), a0);
-  if constexpr (DEPTH == 2) load_a(min(t + stride, ntiles - 1), a1);
-  // epilogue operands one tile ahead (EPF): tile tt's were requested during the previous tile, so their HBM
-  // latency (residual / gelu input rows) hides behind that tile instead of stalling this one's epilogue; the
-  // 9-block-wide and K >= 288 variants have no registers for a second set (they spilled) and load in the tile
-  constexpr bool EPF = NBW == 6 && KC <= 8;
-  uint2 bb[NBW], rr[NBW], ax[NAX];
-  if constexpr (EPF) load_epi(t, bb, rr, ax);
-  auto step = [&](uint4 (&buf)[KC], int tt) {
-    uint4 cur[KC];
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc) cur[kc] = buf[kc];
-    uint2 cb[NBW], cr[NBW], cx[NAX];
-    if constexpr (EPF) {
-#pragma unroll
-      for (int nb = 0; nb < NBW; ++nb) { cb[nb] = bb[nb]; cr[nb] = rr[nb]; }
-#pragma unroll
-      for (int nb = 0; nb < NAX; ++nb) cx[nb] = ax[nb];
-      load_epi(tt + stride, bb, rr, ax);
-    } else {
-      load_epi(tt, cb, cr, cx);
-    }
-    load_a(min(tt + DEPTH * stride, ntiles - 1), buf);
-    process(tt, cur, cb, cr, cx);
-  };
-  for (; t < ntiles; t += DEPTH * stride) {
-    step(a0, t);
-    if constexpr (DEPTH == 2) {
+  if constexpr (RING2) {
+    uint4 a0[KC], a1[KC];
+    uint2 r0[NRR], r1[NRR], x0[NAX], x1[NAX];
+    load_a(min(t, ntiles - 1), a0);
+    load_epi(t, r0, x0);
+    load_a(min(t + stride, ntiles - 1), a1);
+    load_epi(t + stride, r1, x1);
+    for (; t < ntiles; t += 2 * stride) {
+      process(t, a0, r0, x0);
+      load_a(min(t + 2 * stride, ntiles - 1), a0);
+      load_epi(t + 2 * stride, r0, x0);
       __builtin_amdgcn_sched_barrier(0);
-      step(a1, t + stride);
+      process(t + stride, a1, r1, x1);
+      load_a(min(t + 3 * stride, ntiles - 1), a1);
+      load_epi(t + 3 * stride, r1, x1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    uint4 a0[KC];
+    load_a(min(t, ntiles - 1), a0);
+    for (; t < ntiles; t += stride) {
+      uint4 cur[KC];
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) cur[kc] = a0[kc];
+      uint2 rr[NRR], ax[NAX];
+      load_epi(t, rr, ax);
+      load_a(min(t + stride, ntiles - 1), a0);
+      process(t, cur, rr, ax);
     }
   }
 }
@@ -292,9 +290,12 @@ void launch_wres(const dfk_gemm_args& g, int nslices, hipStream_t s) {
   const int ntiles = dfk_cdiv(g.M, 16 * (8 / NSPLIT));
   const int per = std::max(1, std::min(ntiles, 256 * per_cu / nslices));
   const dim3 grid(per * nslices);
-  if (g.act == 1) hipLaunchKernelGGL((wres_kernel<KC, NBW, NSPLIT, 1>), grid, dim3(NT), 0, s, g, nslices, ntiles);
-  else if (g.act == 2) hipLaunchKernelGGL((wres_kernel<KC, NBW, NSPLIT, 2>), grid, dim3(NT), 0, s, g, nslices, ntiles);
-  else hipLaunchKernelGGL((wres_kernel<KC, NBW, NSPLIT, 0>), grid, dim3(NT), 0, s, g, nslices, ntiles);
+#define WRES_L(ACT, RES) hipLaunchKernelGGL((wres_kernel<KC, NBW, NSPLIT, ACT, RES>), grid, dim3(NT), 0, s, g, nslices, ntiles)
+  const bool res = g.residual != nullptr;
+  if (g.act == 1) { if (res) WRES_L(1, true); else WRES_L(1, false); }
+  else if (g.act == 2) { if (res) WRES_L(2, true); else WRES_L(2, false); }
+  else { if (res) WRES_L(0, true); else WRES_L(0, false); }
+#undef WRES_L
 }
 
 bool al8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
