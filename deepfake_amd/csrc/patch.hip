@@ -260,7 +260,12 @@ __global__ __launch_bounds__(NT) void pe_fwd_kernel(const dfk_patch_embed_args a
 }
 
 // Backward, persistent over token rows.  LDS: weight, slab, dconv^T [C][MAXT] and patches^T [96][MAXT]
-// (bf16, the operands of dW = dconv^T . patches over the row's tokens).
+// (bf16, the operands of dW = dconv^T . patches over the row's tokens), the bias / LN gamma (fp32).
+// Software-pipelined like the forward: two register sets hold the clip rows (slab) and the dy / LN-statistics
+// rows of the next two token rows, the loop handles two rows per iteration, and a set is reloaded as soon as
+// its row has consumed it — the loop issues no global store, so the loads' waits stay counted (partial
+// vmcnt).  (The synchronous form — stage the slab, barrier, then load dy, mean, rstd, bias and gamma — paid
+// three exposed memory round trips per row: 472 us per C2 launch.)
 template <int NB>
 __global__ __launch_bounds__(NT) void pe_bwd_kernel(const dfk_patch_embed_args a, const PeGeo g, long nrows,
                                                     const bf16raw* __restrict__ dy) {
@@ -271,11 +276,16 @@ __global__ __launch_bounds__(NT) void pe_bwd_kernel(const dfk_patch_embed_args a
   bf16raw* dcT = w_lds + C * PKS;                  // [C][TS]
   bf16raw* paT = dcT + C * TS;                     // [96][TS]
   float* slab = reinterpret_cast<float*>(paT + PK * TS);
+  float* cb = slab + SROWS * g.Ws;                 // [C] conv bias, [C] LN gamma
+  float* cg = cb + C;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mrow = lane & 15, nq = (lane >> 4) * 4, kq = (lane >> 4) * 8;
   load_weight<NB>(a, w_lds);
-  const bf16raw* gam = reinterpret_cast<const bf16raw*>(a.ln_w);
-  const bf16raw* bias = reinterpret_cast<const bf16raw*>(a.b);
+  {
+    const bf16raw* gam = reinterpret_cast<const bf16raw*>(a.ln_w);
+    const bf16raw* bias = reinterpret_cast<const bf16raw*>(a.b);
+    for (int n = tid; n < C; n += NT) { cb[n] = bf2f(bias[n]); cg[n] = bf2f(gam[n]); }
+  }
   float dgam[NB][4], dbet[NB][4], dbia[NB][4];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb)
@@ -285,11 +295,20 @@ __global__ __launch_bounds__(NT) void pe_bwd_kernel(const dfk_patch_embed_args a
 #pragma unroll
   for (int i = 0; i < TPW; ++i) dw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (long row = blockIdx.x; row < nrows; row += gridDim.x) {
-    __syncthreads();                                 // previous row's LDS reads are done
-    stage_slab(a, g, row, slab);
-    __syncthreads();
-    const long tok0 = row * g.Wo;
+  const int w = wave * 16 + mrow;
+  const bool wok = w < g.Wo;
+  const int wc = wok ? w : 0;
+  // this lane's dy channels and the token's LN statistics for token row `row` (rows past the end: clamped;
+  // their values are never used)
+  struct RowOps { uint2 d[NB]; float mean, rstd; };
+  auto load_ops = [&](long row, RowOps& o) {
+    const long tok = (row < nrows ? row : nrows - 1) * g.Wo + wc;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) o.d[nb] = *reinterpret_cast<const uint2*>(dy + tok * C + nb * 16 + nq);
+    o.mean = a.mean[tok];
+    o.rstd = a.rstd[tok];
+  };
+  auto compute = [&](const RowOps& o) {
     // patches^T [k][token] (zero for tokens past Wo)
     for (int i = tid; i < PK * MAXT; i += NT) {
       const int k = i / MAXT, m = i % MAXT;
@@ -297,24 +316,21 @@ __global__ __launch_bounds__(NT) void pe_bwd_kernel(const dfk_patch_embed_args a
       if (m < g.Wo) v = slab[(k >> 2) * g.Ws + m * 4 + (k & 3)];
       paT[k * TS + m] = f2bf(v);
     }
-    const int w = wave * 16 + mrow;
-    const bool wok = w < g.Wo;
     f32x4 acc[NB];
-    conv_tokens<NB>(slab, g.Ws, w_lds, wok ? w : 0, acc);
-    const float mean = wok ? a.mean[tok0 + w] : 0.f, rstd = wok ? a.rstd[tok0 + w] : 0.f;
+    conv_tokens<NB>(slab, g.Ws, w_lds, wc, acc);
+    const float mean = wok ? o.mean : 0.f, rstd = wok ? o.rstd : 0.f;
     float xh[NB][4], gg[NB][4], dyv[NB][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const int n = nb * 16 + nq;
-      uint2 u = make_uint2(0, 0);
-      if (wok) u = *reinterpret_cast<const uint2*>(dy + (tok0 + w) * C + n);
+      const uint2 u = wok ? o.d[nb] : make_uint2(0, 0);
       dyv[nb][0] = __uint_as_float(u.x << 16); dyv[nb][1] = __uint_as_float(u.x & 0xffff0000u);
       dyv[nb][2] = __uint_as_float(u.y << 16); dyv[nb][3] = __uint_as_float(u.y & 0xffff0000u);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        xh[nb][r] = (acc[nb][r] + bf2f(bias[n + r]) - mean) * rstd;
-        gg[nb][r] = dyv[nb][r] * bf2f(gam[n + r]);
+        xh[nb][r] = (acc[nb][r] + cb[n + r] - mean) * rstd;
+        gg[nb][r] = dyv[nb][r] * cg[n + r];
         s1 += gg[nb][r];
         s2 += gg[nb][r] * xh[nb][r];
       }
@@ -342,6 +358,29 @@ __global__ __launch_bounds__(NT) void pe_bwd_kernel(const dfk_patch_embed_args a
         dw[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, dw[i], 0, 0, 0);
       }
     }
+  };
+  const long G = gridDim.x;
+  long row = blockIdx.x;
+  float4 s0[SLAB_REGS], s1[SLAB_REGS];
+  RowOps o0, o1;
+  slab_load(a, g, row, s0);                        // rows past the end read zeros (out-of-range offsets)
+  load_ops(row, o0);
+  slab_load(a, g, row + G, s1);
+  load_ops(row + G, o1);
+  // one row per half-iteration: store its slab, reload that register set for the row two ahead, compute
+  auto half = [&](float4 (&sr)[SLAB_REGS], RowOps& o) {
+    __syncthreads();                               // the previous row's LDS reads are done
+    slab_store(g, sr, slab);
+    __syncthreads();
+    slab_load(a, g, row + 2 * G, sr);
+    compute(o);
+    load_ops(row + 2 * G, o);
+    row += G;
+  };
+  while (row < nrows) {
+    half(s0, o0);
+    if (row >= nrows) break;
+    half(s1, o1);
   }
   // ---- one atomic per weight (and per LN / bias channel) per workgroup
 #pragma unroll
@@ -387,7 +426,7 @@ bool pe_geo(const dfk_patch_embed_args& a, PeGeo& g) {
 
 size_t pe_lds_fwd(int C, const PeGeo& g) { return (size_t)C * PKS * 2 + 4 * 16 * (C + 8) * 2 + (size_t)SROWS * g.Ws * 4; }
 size_t pe_lds_bwd(int C, const PeGeo& g) {
-  return (size_t)C * PKS * 2 + (size_t)(C + PK) * (MAXT + 8) * 2 + (size_t)SROWS * g.Ws * 4;
+  return (size_t)C * PKS * 2 + (size_t)(C + PK) * (MAXT + 8) * 2 + (size_t)SROWS * g.Ws * 4 + (size_t)C * 8;
 }
 
 }  // namespace
@@ -438,7 +477,8 @@ extern "C" int dfk_patch_embed_bwd(const dfk_patch_embed_args* ap, const void* d
     (void)hipFuncSetAttribute((const void*)pe_bwd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  const unsigned grid = (unsigned)std::min<long>(rows, 512);
+  // one workgroup per CU (the kernel's VGPR + AGPR budget leaves one wave per SIMD), persistent over rows
+  const unsigned grid = (unsigned)std::min<long>(rows, 256);
   if (a.C == 96)
     hipLaunchKernelGGL(pe_bwd_kernel<6>, dim3(grid), dim3(NT), lds, s, a, g, rows, (const bf16raw*)dy);
   else
