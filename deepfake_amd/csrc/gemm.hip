@@ -834,7 +834,10 @@ void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int eve
     else dispatch_dma_conv<64>(g, grid, kchunk, evec, sk, s);
     return;
   }
-  const int st = dma_stages(wt);
+  // weight gradients (k-major A: the token dimension is the reduction) on 128x128 tiles: tuning knob for their ring
+  // depth (3 stages measured slower: dW 116 -> 119 us, C2 256.8 -> 247.7 clips/s, profiles/gemm/r4sdw_*)
+  static const int sdw = getenv("DFK_DMA_SDW") ? atoi(getenv("DFK_DMA_SDW")) : 2;
+  const int st = g.a_kmajor && wt == 64 ? sdw : dma_stages(wt);
   if (wt == 33) {   // 128 x 64 (8 waves of 32 x 32)
     dispatch_dma_s<32, 4, 2, 2>(g, grid, kchunk, evec, sk, s);
     return;
