@@ -14,7 +14,7 @@ from . import _lib as L
 # split-K target grid of a skinny weight-gradient GEMM: 256 workgroups.  In isolation 512 (two per CU) runs each
 # dW fastest, but inside the step the other two branch streams fill the chip and fewer splits mean fewer fp32
 # partials (whole-step A/B, C2: 512 / 256 / 128 = 241.7 / 244.8 / 245.3 clips/s, 64: 232.7; C4 Swin-B:
-# 134.1 / 133.1 / 124.3 — 256 holds both)
+# 134.1 / 133.1 / 124.3 — 256 holds both; round 4, r4tg: C2 160 / 256 = 257.9 / 256.7, C4 134.1 / 139.2)
 _CU_TARGET_BLOCKS = int(os.environ.get("DFK_DW_TARGET", "256"))
 
 
