@@ -79,6 +79,17 @@ def test_linear_weight_resident(M, N, Kd):
     aux2 = torch.randn(M, Kd, device=DEV, generator=g).to(dt)
     ref2 = (dy.float() @ w.float()) * torch.func.grad(lambda t: torch.nn.functional.gelu(t).sum())(aux2.float())
     assert rel(K.linear_dx(dy, w, act=2, aux=aux2), ref2) < tol(dt)
+    # absent bias (the bias tile in LDS is zero) into an output pre-filled with NaN (no epilogue reads it), GELU
+    # with a residual, and dGELU with a residual (the skip-path gradient) — the RES / ACT template pairs
+    nobias = x.float() @ w.float().t()
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=dt)
+    assert rel(K.linear(x, w, None, out=out), nobias) < tol(dt)
+    aux3 = torch.full((M, N), float("nan"), device=DEV, dtype=dt)
+    y3 = K.linear(x, w, None, act=1, aux=aux3, residual=r)
+    assert rel(aux3, nobias) < tol(dt)
+    assert rel(y3, torch.nn.functional.gelu(nobias) + r.float()) < tol(dt)
+    r2 = torch.randn(M, Kd, device=DEV, generator=g).to(dt)
+    assert rel(K.linear_dx(dy, w, act=2, aux=aux2, residual=r2), ref2 + r2.float()) < tol(dt)
 
 
 @pytest.mark.parametrize("M,N,Kd", [(20000, 288, 96), (16500, 96, 96), (17000, 384, 96), (16400, 96, 384),
