@@ -630,16 +630,26 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / NWN, wn = wave % NWN;
-  int tn, tmi;
-  {
-    const int nwg = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+  int tn, tmi, z;
+  const int nwg = gridDim.x * gridDim.y;
+  if (g.atomic && g.splitk % 8 == 0 && (int)gridDim.z == g.splitk && nwg > 1) {
+    // atomic split-K weight gradients: all nwg output tiles of one split on one XCD (the dispatcher deals
+    // workgroups of the linear order to the 8 XCDs round robin), so the token range of the operand every tile
+    // of that split reads (x: the whole narrow dW row block) comes from that XCD's L2 after the first tile
+    const int lin = blockIdx.z * nwg + blockIdx.y * gridDim.x + blockIdx.x;
+    const int j = lin >> 3, i = j % nwg;
+    z = (j / nwg) * 8 + (lin & 7);
+    tn = i % gridDim.x;
+    tmi = i / gridDim.x;
+  } else {
+    const int bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
     const int nid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
     tn = nid % gridDim.x;
     tmi = nid / gridDim.x;
+    z = blockIdx.z;
   }
   const int bn = tn * BN, bm = tmi * BM;
-  int z = blockIdx.z;
   const int split = z % g.splitk;
   z /= g.splitk;
   const int z0 = z / g.nz1, z1 = z % g.nz1;

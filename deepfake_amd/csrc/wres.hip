@@ -66,7 +66,16 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   bf16raw* stg = w_lds + BN * WS + wave * 16 * SS;
   const int rg = wave / NSPLIT, cg = wave % NSPLIT;
-  const int slice = blockIdx.x % nslices;
+  // block -> (column slice, first tile).  When the grid is a multiple of 8 x nslices, the nslices slices of one
+  // row tile are blocks b, b + 8, b + 16, ... — one XCD (blocks are dealt to the 8 XCDs round robin) — so the
+  // A rows they all read come from that XCD's L2 after the first; otherwise slice-major as before
+#ifndef DFK_WRES_XCD
+#define DFK_WRES_XCD 1
+#endif
+  const bool xcd_map = DFK_WRES_XCD && nslices > 1 && gridDim.x % (8 * nslices) == 0;
+  const int bj = blockIdx.x >> 3;
+  const int slice = xcd_map ? bj % nslices : blockIdx.x % nslices;
+  const int t_first = xcd_map ? (bj / nslices) * 8 + (blockIdx.x & 7) : blockIdx.x / nslices;
   const int n0 = slice * BN;
   const int stride = gridDim.x / nslices;
   const bf16raw* W = reinterpret_cast<const bf16raw*>(g.b.ptr);
@@ -252,7 +261,7 @@ void wres_kernel(const dfk_gemm_args g, int nslices, int ntiles) {
   // clamped loads and its stores fall outside the output descriptor (rows >= M): no branch surrounds a load or
   // a store.
   constexpr bool RING2 = (NBW == 6 ? KC <= 8 : KC <= DFK_WRES_R9) && !wres_two_per_cu<KC, NBW, NSPLIT>();
-  int t = blockIdx.x / nslices;
+  int t = t_first;
   if constexpr (RING2) {
     uint4 a0[KC], a1[KC];
     uint2 r0[NRR], r1[NRR], x0[NAX], x1[NAX];

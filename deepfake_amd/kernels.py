@@ -175,6 +175,7 @@ def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None, residual=No
 
 
 _DW_MIN_K = int(os.environ.get("DFK_DW_MINK", "512"))   # tokens per split of a weight-gradient GEMM (tuning)
+_DW_XCD = int(os.environ.get("DFK_DW_XCD", "1"))   # split counts rounded to multiples of 8 (XCD grouping; A/B knob)
 
 
 def splitk_for(tiles, K, min_k=None):
@@ -197,6 +198,8 @@ def linear_dw(dy, x, dw, db=None):
     # fp32 partial bytes (splits x N x K x 4) kept to a quarter of the operand bytes read, except that small
     # grids keep up to 8 splits for parallelism (C2 sweep: mel1.fc1 [25088]x512x128 98 -> 30 splits, 42 -> 28 us)
     s = max(1, min(s, max(8, M * (N + K) // (8 * N * K))))
+    if _DW_XCD and tiles > 1 and s >= 16:
+        s -= s % 8   # a multiple of 8 splits: the kernel puts each split's tiles on one XCD (shared operand in L2)
     gemm(dy, dy.stride(0), True, x, x.stride(0), True, N, K, M, dw, dw.stride(0), dtype=L.dt(dy), c_f32=True,
          atomic=s > 1, beta=1.0, splitk=s, rowsum=db)
     return dw
