@@ -104,6 +104,7 @@ SIGNATURES = {
     "dfk_wattn_fwd": [C.POINTER(WattnArgs), _VP],
     "dfk_wattn_bwd": [C.POINTER(WattnBwdArgs), _VP],
     "dfk_wattn_bwd_workspace": [C.POINTER(WattnArgs)],
+    "dfk_wattn_fwd_policy": [C.c_int32, C.c_int64],
     "dfk_wattn_table_workspace": [C.POINTER(WattnArgs)],
     "dfk_wattn_table": [C.POINTER(WattnArgs), _VP],
     "dfk_patch_im2col": [_VP, C.c_int, _VP, C.c_int, C.POINTER(Im2colArgs), _VP],
@@ -115,11 +116,13 @@ SIGNATURES = {
     "dfk_cosine_qk_bwd": [_VP, _VP, _VP, _VP, _F, _VP, _I64, C.c_int, C.c_int, C.c_int, _VP],
     "dfk_cpb_bias_fwd": [_VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],
     "dfk_cpb_bias_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],
+    "dfk_cpb_bias_fwd_many": [_VP, _I32, _I32, _VP, _VP],
+    "dfk_cpb_bias_bwd_many": [_VP, _I32, _I32, _VP, _VP, _VP],
     "dfk_w2v_conv0_fwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _VP],
     "dfk_w2v_conv0_fwd_workspace": [_I64, _I64],
     "dfk_w2v_conv0_bwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _I64, _VP, _VP, _VP, _VP],
     "dfk_w2v_conv0_bwd_workspace": [_I64, _I64],
-    "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP, _VP],
+    "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP, _F, _VP, _VP],
     "dfk_im2col2d": [_VP, _I64, _VP, C.POINTER(Conv2dGeo), C.c_int, _VP],
     "dfk_col2im2d": [_VP, _VP, _I64, C.POINTER(Conv2dGeo), C.c_int, C.c_int, _VP],
     "dfk_bn2d_fwd": [_VP, _I64, _VP, _I64, _I64, _I32, _VP, _VP, _F, _F, C.c_int, _VP, _VP, _VP, _VP, _VP, C.c_int,

@@ -144,24 +144,35 @@ __global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, long n
 //   g = grad + wd*p ; buf = first ? g : mom*buf + g ; p -= lr*buf ; shadow = bf16(p)
 // NT: the parameter / momentum / shadow stores are non-temporal (streamed to HBM, not left dirty in L2 / MALL),
 // so that their write-back does not land on the first kernels of the next step (the clip-batch patch embedding)
+// Data-parallel fold (gscale, gbf): the gradient read is the all-reduced SUM — the fp32 buffer itself, or the
+// bf16 bucket copy RCCL summed (gbf != NULL) — times gscale = 1 / world, so no separate averaging / cast-back
+// pass over the flat gradient runs between the last all-reduce and the step (ddp.py GradBucketer.finish(fold)).
 template <bool NT>
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ grad, float* __restrict__ buf,
                            bf16raw* __restrict__ shadow, long n, const float* __restrict__ lr_dev, float lr_host,
-                           float mom, float wd, int first, const float* __restrict__ gate) {
+                           float mom, float wd, int first, const float* __restrict__ gate, float gscale,
+                           const bf16raw* __restrict__ gbf) {
   const long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i0 >= n) return;
   if (gate && *gate == 0.f) return;   // LayerDrop-skipped layer: torch's SGD skips grad=None parameters
   const float lr = lr_dev ? *lr_dev : lr_host;
   if (i0 + 4 <= n) {
     float4 pv = *reinterpret_cast<float4*>(p + i0);
-    const float4 gv = *reinterpret_cast<const float4*>(grad + i0);
+    float4 gv;
+    if (gbf) {
+      const uint2 u = *reinterpret_cast<const uint2*>(gbf + i0);
+      gv = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xffff0000u));
+    } else {
+      gv = *reinterpret_cast<const float4*>(grad + i0);
+    }
     float4 bv = first ? make_float4(0, 0, 0, 0) : *reinterpret_cast<float4*>(buf + i0);
     float* pp = reinterpret_cast<float*>(&pv);
     const float* gg = reinterpret_cast<const float*>(&gv);
     float* bb = reinterpret_cast<float*>(&bv);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float g = gg[k] + wd * pp[k];
+      const float g = gg[k] * gscale + wd * pp[k];
       bb[k] = first ? g : mom * bb[k] + g;
       pp[k] -= lr * bb[k];
     }
@@ -183,7 +194,7 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ grad
     }
   } else {
     for (long i = i0; i < n; ++i) {
-      const float g = grad[i] + wd * p[i];
+      const float g = (gbf ? bf2f(gbf[i]) : grad[i]) * gscale + wd * p[i];
       buf[i] = first ? g : mom * buf[i] + g;
       p[i] -= lr * buf[i];
       if (shadow) shadow[i] = f2bf(p[i]);
@@ -423,11 +434,12 @@ extern "C" int dfk_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_
 
 extern "C" int dfk_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow, int64_t n,
                             const float* lr_dev, float lr, float momentum, float weight_decay, int first_step,
-                            const float* gate, hipStream_t s) {
+                            const float* gate, float grad_scale, const void* grad_bf16, hipStream_t s) {
   if (!param || !grad || !momentum_buf) return DFK_EINVAL;
   if ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
        reinterpret_cast<uintptr_t>(momentum_buf)) & 15)
     return DFK_EINVAL;
+  if (reinterpret_cast<uintptr_t>(grad_bf16) & 7) return DFK_EINVAL;
   if (n <= 0) return 0;
   const long threads = (n + 3) / 4;
   // DFK_SGD_NT=1: non-temporal stores (A/B runs; no measurable effect on the step or on the next step's patch
@@ -435,7 +447,8 @@ extern "C" int dfk_sgd_step(float* param, const float* grad, float* momentum_buf
   static const bool nt = getenv("DFK_SGD_NT") && atoi(getenv("DFK_SGD_NT")) != 0;
   auto kfn = nt ? sgd_kernel<true> : sgd_kernel<false>;
   hipLaunchKernelGGL(kfn, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, param, grad, momentum_buf,
-                     (bf16raw*)bf16_shadow, (long)n, lr_dev, lr, momentum, weight_decay, first_step, gate);
+                     (bf16raw*)bf16_shadow, (long)n, lr_dev, lr, momentum, weight_decay, first_step, gate, grad_scale,
+                     (const bf16raw*)grad_bf16);
   DFK_CHECK_LAUNCH();
   return 0;
 }

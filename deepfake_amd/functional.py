@@ -641,6 +641,75 @@ class CPBBiasFn(torch.autograd.Function):
         return None, grad_done(w1, d1), grad_done(b1, db), grad_done(w2, d2)
 
 
+_CPB_DESC = {}   # (pointers, dims) -> device descriptor array of dfk_cpb_bias_*_many (built once, replay-safe)
+
+
+def _cpb_desc(rows):
+    key = tuple(tuple(r) for r in rows)
+    d = _CPB_DESC.get(key)
+    if d is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("cpb descriptor built inside a graph capture (run one eager step first)")
+        d = torch.tensor([v for r in rows for v in r], dtype=torch.int64).cuda()
+        if len(_CPB_DESC) > 64:   # modules without a ParamStore get fresh gradient buffers every call
+            _CPB_DESC.clear()
+        _CPB_DESC[key] = d
+    return d
+
+
+class CPBManyFn(torch.autograd.Function):
+    """Every SwinV2 block's relative-position bias table 16*sigmoid(cpb_mlp(coords)) (swin_transformer2d.py:159-162)
+    in ONE launch forward (dfk_cpb_bias_fwd_many) and one backward (dfk_cpb_bias_bwd_many) — the tables depend on
+    parameters only, so the 24 blocks of SwinV2-B need not pay 24 launches each way.  Inputs: the coordinate tables,
+    then (w1, b1, w2) of every block; outputs: the [L, heads] tables (views of one fp32 buffer)."""
+
+    @staticmethod
+    def forward(ctx, n, *ts):
+        coords, params = ts[:n], ts[n:]
+        cs = [c.detach().float().reshape(-1, 2).contiguous() for c in coords]
+        ws = [p.detach().float().contiguous() for p in params]
+        dims, off, fwd_rows = [], 0, []
+        for i in range(n):
+            w1, b1, w2 = ws[3 * i:3 * i + 3]
+            L, heads, hidden = cs[i].shape[0], w2.shape[0], w2.shape[1]
+            assert heads <= 32, heads
+            dims.append((off, L, heads))
+            base = [cs[i].data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr()]
+            fwd_rows.append(base + [0, 0, 0, off, L, hidden, heads, 0])
+            off += L * heads
+        out = torch.empty(off, device=cs[0].device, dtype=torch.float32)
+        maxL = max(d[1] for d in dims)
+        K.L.check(K.L.lib().dfk_cpb_bias_fwd_many(K.L.ptr(_cpb_desc(fwd_rows)), n, maxL, K.L.ptr(out),
+                                                   K.L.stream()), "cpb_bias_fwd_many")
+        for i, p in enumerate(params):
+            grad_use(ctx, 1 + n + i, p)
+        ctx.n, ctx.dims, ctx.maxL, ctx.fwd_rows = n, dims, maxL, fwd_rows
+        ctx.save_for_backward(out, *cs, *ws, *params)   # cs / ws: the descriptor's pointers stay valid
+        return tuple(out[o:o + L * h].view(L, h) for o, L, h in dims)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        saved = ctx.saved_tensors
+        n = ctx.n
+        out, params = saved[0], saved[1 + n + 3 * n:]
+        dflat = torch.cat([(d if d is not None else torch.zeros(L, h, device=out.device)).float().reshape(-1)
+                           for d, (o, L, h) in zip(douts, ctx.dims)])
+        sinks = [grad_sink(p) for p in params]
+        rows = [r[:4] + [t.data_ptr() for t in sinks[3 * i:3 * i + 3]] + r[7:] for i, r in enumerate(ctx.fwd_rows)]
+        K.L.check(K.L.lib().dfk_cpb_bias_bwd_many(K.L.ptr(_cpb_desc(rows)), n, ctx.maxL, K.L.ptr(out),
+                                                   K.L.ptr(dflat), K.L.stream()), "cpb_bias_bwd_many")
+        return (None,) + (None,) * n + tuple(grad_done(p, g) for p, g in zip(params, sinks))
+
+
+def cpb_tables(attns):
+    """The bias tables of a list of SwinV2 WindowAttention modules in one launch each way (CPBManyFn)."""
+    coords = [a.relative_coords_table for a in attns]
+    params = []
+    for a in attns:
+        params += [a.cpb_mlp[0].weight, a.cpb_mlp[0].bias, a.cpb_mlp[2].weight]
+    return CPBManyFn.apply(len(attns), *coords, *params)
+
+
 class PatchEmbedLNFn(torch.autograd.Function):
     """Fused PatchEmbed3D pad + Conv3d(2x4x4) + LayerNorm in bf16 (video_swin_transformer.py:446-458):
     dfk_patch_embed_fwd reads the fp32 clip once and writes the normalised bf16 tokens once; the backward

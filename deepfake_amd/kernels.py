@@ -314,6 +314,12 @@ def wattn_fwd(q, k, v, ld_qkv, dims, window, full_window, shift, heads, hd, scal
     return out, lse
 
 
+def wattn_fwd_policy(version=-1, bal_min_units=-1):
+    """Process-wide kernel choice of the hd-32 bf16 table forward (tests / A/B runs): version 5 (no running max,
+    default) or 4; bal_min_units = smallest launch on the balanced key-split schedule. -1 leaves a setting."""
+    L.check(L.lib().dfk_wattn_fwd_policy(int(version), int(bal_min_units)), "wattn_fwd_policy")
+
+
 def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None, mask=None, tab=None, drop=None):
     """Backward of wattn_fwd.  fwd_args_tensors = (q, k, v, out, lse, ld_qkv, dims, window, full_window,
     shift, heads, hd, scale, rpb, pads).  dq/dk/dv may alias column slices of one [rows, 3C] buffer."""
@@ -485,10 +491,13 @@ def wave_normalize(wave, eps=1e-7):
     return out
 
 
-def sgd_step(param, grad, buf, shadow, lr, momentum, wd, first, lr_dev=None, gate=None):
+def sgd_step(param, grad, buf, shadow, lr, momentum, wd, first, lr_dev=None, gate=None, grad_scale=1.0,
+             grad_bf16=None):
+    """grad_scale / grad_bf16: the data-parallel fold (gradient = grad_bf16 or grad, times grad_scale)."""
     L.check(L.lib().dfk_sgd_step(L.ptr(param), L.ptr(grad), L.ptr(buf), L.ptr(shadow) if shadow is not None else None,
                                  param.numel(), L.ptr(lr_dev) if lr_dev is not None else None, float(lr),
-                                 float(momentum), float(wd), int(first), L.ptr(gate), L.stream()), "sgd_step")
+                                 float(momentum), float(wd), int(first), L.ptr(gate), float(grad_scale),
+                                 L.ptr(grad_bf16) if grad_bf16 is not None else None, L.stream()), "sgd_step")
 
 
 def dropout(x, drop, out=None, group_rows=None):

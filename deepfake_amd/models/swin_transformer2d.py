@@ -10,6 +10,7 @@ normalised, q scaled by exp(clamp(logit_scale))) + window attention with the
 x + LN(attn(x)), x + LN(mlp(x)) (:288-291).
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -120,7 +121,8 @@ class WindowAttention(nn.Module):
         geo = (dims, (1, ws, ws), (1, self.window_size[0], self.window_size[1]), (0, shift, shift),
                self.num_heads, hd, 1.0)
         ad = self.attn_drop.spec() if self.attn_drop is not None and self.training else None
-        out = Fn.window_attention(qkv, self.bias_table(), None, geo, drop=ad)
+        tab = self._cpb if getattr(self, "_cpb", None) is not None else self.bias_table()
+        out = Fn.window_attention(qkv, tab, None, geo, drop=ad)
         return (out, xs) if skip else out
 
 
@@ -290,8 +292,18 @@ class SwinTransformerV2(nn.Module):
 
     def forward_features(self, x):
         x = self.patch_embed(x)
-        for layer in self.layers:
-            x = layer(x)
+        # every block's CPB table in one launch each way (parameters only; Fn.cpb_tables), handed to the blocks
+        # for this forward only
+        attns = [blk.attn for layer in self.layers for blk in layer.blocks]
+        if x.is_cuda and os.environ.get("DFK_CPB_MANY", "1") != "0":
+            for a, t in zip(attns, Fn.cpb_tables(attns)):
+                a._cpb = t
+        try:
+            for layer in self.layers:
+                x = layer(x)
+        finally:
+            for a in attns:
+                a._cpb = None
         B, L, C = x.shape
         x = Fn.layer_norm(x, self.norm)
         return Fn.RowMeanFn.apply(x.reshape(B * L, C), B)

@@ -27,9 +27,11 @@ class FusedSGD:
         self.param_groups[0]["lr"] = float(lr)
         self.lr_dev.fill_(float(lr))
 
-    def step(self, first=None):
+    def step(self, first=None, grad_scale=1.0, grad_bf16=None):
         """One SGD step over the parameters that received a gradient (torch skips grad=None:
-        no weight decay and no momentum for them), in as few contiguous launches as possible."""
+        no weight decay and no momentum for them), in as few contiguous launches as possible.
+        grad_scale / grad_bf16: the data-parallel fold of GradBucketer.finish(fold=True) — the gradient is the
+        all-reduced sum (in the fp32 buffer, or in the bf16 bucket copy) times 1 / world."""
         st = self.store
         gates = {id(g): g for g in st.gate if g is not None}
         gkey = [id(g) if g is not None else None for g in st.gate]
@@ -44,7 +46,8 @@ class FusedSGD:
         # a LayerDrop-gated run is skipped on the device when its layer was dropped this step
         for s, e, (f, k) in runs:
             K.sgd_step(st.flat[s:e], st.grad[s:e], self.buf[s:e], st.shadow[s:e] if st.shadow is not None else None,
-                       0.0, self.momentum, self.weight_decay, bool(f), lr_dev=self.lr_dev, gate=gates.get(k))
+                       0.0, self.momentum, self.weight_decay, bool(f), lr_dev=self.lr_dev, gate=gates.get(k),
+                       grad_scale=grad_scale, grad_bf16=grad_bf16[s:e] if grad_bf16 is not None else None)
         self.first = False
 
     def zero_grad(self):

@@ -49,11 +49,21 @@ def normalize_wave(w):
     return K.wave_normalize(w)
 
 
-def check_finite(loss, step):
+def check_finite(loss, step, group=None, device="cpu"):
     """Failure detection at log steps (the only host sync of the loop): a NaN / Inf loss stops training with an
     error instead of stepping SGD on garbage.  The attention kernels are built without NaN semantics
-    (build.py), so a diverging run is caught here, at the loss, not inside the kernels."""
-    if not math.isfinite(loss):
+    (build.py), so a diverging run is caught here, at the loss, not inside the kernels.
+    Data-parallel (group given): the loss is rank-local while the gradients are averaged, so one rank's bad
+    batch must not make that rank alone raise while the others block in the next bucket all-reduce until the
+    RCCL watchdog fires — the non-finite flag is MAX-all-reduced and every rank raises at the same step."""
+    bad = not math.isfinite(loss)
+    if group is not None:
+        flag = torch.tensor([1.0 if bad else 0.0], device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if flag.item() > 0 and not bad:
+            raise FloatingPointError(f"non-finite training loss on another rank at optimizer step {step} "
+                                     f"(this rank: {loss})")
+    if bad:
         raise FloatingPointError(f"non-finite training loss {loss} at optimizer step {step}")
     return loss
 
@@ -152,12 +162,17 @@ class TrainStep:
                 loss, prob = self._fwd_bwd(feature, label, 1.0 / accum)
             return loss.detach(), prob.detach()
         loss, prob = self._fwd_bwd(feature, label, 1.0 / accum)
-        self.bucketer.finish()          # overlapped bucket all-reduces (hooks), then average
-        self.opt.step()                 # first call initialises the momentum buffer (torch SGD semantics)
+        fold = self._fold()
+        fa = self.bucketer.finish(fold=fold)   # overlapped bucket all-reduces (hooks); the mean is taken by SGD
+        self.opt.step(**fa)             # first call initialises the momentum buffer (torch SGD semantics)
         self.store.zero_grad()
         self.first_micro = True
         # detach: a live autograd graph would pin AccumulateGrad nodes to this stream (breaks capture)
         return loss.detach(), prob.detach()
+
+    def _fold(self):
+        """The fused SGD kernel takes the all-reduced sum and the 1 / world scale itself (no averaging pass)."""
+        return isinstance(self.opt, FusedSGD)
 
     def eager(self, feature, label):
         return self._micro_eager(feature, label, True, 1)
@@ -287,11 +302,12 @@ class TrainStep:
                 if bn:
                     self.bucketer.broadcast_bn()
             l2, p2 = self._fwd_bwd(tuple(static_in), static_label, 1.0 / accum)
+            fold = self._fold()
             if overlap:
-                self.bucketer.finish()         # flush unused buckets, join the comm stream, average
+                fa = self.bucketer.finish(fold=fold)   # flush unused buckets, join the comm stream
             else:
-                self.bucketer.allreduce_all()
-            self.opt.step(first=False)
+                fa = self.bucketer.allreduce_all(fold=fold)
+            self.opt.step(first=False, **fa)
             if accum > 1:                      # the next window starts from zero gradients and gates
                 self.store.grad.zero_()
                 self.store.zero_gates()
@@ -476,7 +492,8 @@ class Trainer:
                     self.scheduler.step()
                     if t % self.log_step == 0:
                         li = loss.item()
-                        check_finite(li, t)
+                        check_finite(li, t, (self.bucketer.group or dist.group.WORLD) if self.bucketer.enabled
+                                     else None, self.store.grad.device)
                         stat.update(li)
                         dt = time.time() - t0
                         self.logger("| epoch {:2d} | step {:4d} | lr {:.4E} | Train Loss Avg {:3.5f} | clips/s {:.2f}"

@@ -202,6 +202,11 @@ typedef struct {
                            nn.functional.dropout(attn_weights, p=attention_dropout) (HF :458) */
 } dfk_wattn_args;
 int dfk_wattn_fwd(const dfk_wattn_args* a, hipStream_t stream);
+/* kernel-selection policy of dfk_wattn_fwd's hd-32 table path (process-wide; tests and A/B runs only — the
+ * defaults are the product's choice): version 5 = no-running-max forward (default), 4 = the max-subtracted
+ * forward; bal_min_units = smallest launch (units = clips x windows x heads) that runs the key-split balanced
+ * schedule (default 512).  A negative argument leaves that setting unchanged.  Returns 0. */
+int dfk_wattn_fwd_policy(int32_t version, int64_t bal_min_units);
 int64_t dfk_wattn_table_workspace(const dfk_wattn_args* a);
 /* builds a->tab (fwd and bwd layouts) from a->rpb, the shift and the window geometry
  * (replaces the RPB gather + mask add of WindowAttention3D.forward, :152-163) */
@@ -317,6 +322,13 @@ int dfk_cpb_bias_fwd(const float* coords, const float* w1, const float* b1, cons
 int dfk_cpb_bias_bwd(const float* coords, const float* w1, const float* b1, const float* w2, const float* out,
                      const float* dout, float* dw1, float* db1, float* dw2, int32_t L, int32_t hidden, int32_t heads,
                      hipStream_t stream);
+/* every SwinV2 block's table in one launch each way (the 24 blocks of SwinV2-B: 48 launches -> 2).  desc: DEVICE
+ * array of n records of 12 int64 {coords, w1, b1, w2, dw1, db1, dw2 (device pointers; the gradients are
+ * accumulated with fp32 atomics), off (float offset of the block's [L, heads] table in out / dout), L, hidden,
+ * heads (<= 32), 0}; max_L >= every record's L.  Same arithmetic per table as dfk_cpb_bias_fwd / _bwd. */
+int dfk_cpb_bias_fwd_many(const int64_t* desc, int32_t n, int32_t max_L, float* out, hipStream_t stream);
+int dfk_cpb_bias_bwd_many(const int64_t* desc, int32_t n, int32_t max_L, const float* out, const float* dout,
+                          hipStream_t stream);
 
 /* dx = dy * gelu'(pre) (exact-erf GELU backward, torch nn.GELU / HF ACT2FN["gelu"]). */
 int dfk_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, int dtype, hipStream_t stream);
@@ -327,10 +339,13 @@ int dfk_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, int dtype
  * memory when lr_dev != NULL (graph-replay safe CosineAnnealingLR). */
 int dfk_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow, int64_t n,
                  const float* lr_dev, float lr, float momentum, float weight_decay, int first_step,
-                 const float* gate, hipStream_t stream);
+                 const float* gate, float grad_scale, const void* grad_bf16, hipStream_t stream);
 /* gate (above; may be NULL): device flag, the step is skipped when *gate == 0 — the parameters of a
  * LayerDrop-skipped wav2vec2 layer have grad None in the reference and torch's SGD leaves them (and
- * their momentum) untouched. */
+ * their momentum) untouched.
+ * grad_scale multiplies the gradient read (1 / world: the data-parallel mean of the all-reduced sum,
+ * DataParallel's averaging of src/trainer.py:74-75 folded into the step); grad_bf16 (NULL, or 8-B aligned):
+ * read the gradient from this bf16 buffer (the all-reduced bf16 bucket copy) instead of `grad`. */
 
 /* y = x * mask / (1 - p) over [rows, cols] (row stride ld; y may alias x): nn.Dropout / DropPath as a
  * standalone pass, and the backward of every fused dropout site (the same mask applied to the gradient). */

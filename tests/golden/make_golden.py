@@ -335,6 +335,52 @@ def case_fused_c2():
     save(c["name"], _big=GC.GRAD_SAMPLE_C2, _sample=GC.GRAD_SAMPLE_C2, **out)
 
 
+def case_fused_c2_fp8():
+    """The anchor of C4's fp8 gradient bounds: the reference fused C2 model's training step in fp32 with its
+    video stage-3/4 qkv / proj / fc1 / fc2 Linears on MX-fp8 operands emulated (tests/mx_ref.MXLinearFn: forward
+    and input-gradient operands fake-quantised, weight gradients unquantised — what models.set_fp8 runs), against
+    the same step unquantised.  ``ef8:<param>`` is that gradient error in the parity metric (tests/fixtures.error),
+    z / loss the emulated run's logits and loss."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import mx_ref
+    c = GC.FUSED_C2
+    video, mel, wave, label = synthetic_inputs(c["B"], c["T"], c["H"], c["W"], c["seconds"], seed=c["seed"] + 1)
+    grads, outs = [], []
+    for emulate in (False, True):
+        m = build_fused_ref(c)
+        named_fill_(m, seed=c["seed"])
+        if emulate:
+            n = 0
+            for li in (2, 3):
+                for blk in m.vExtract.vst.layers[li].blocks:
+                    for lin in (blk.attn.qkv, blk.attn.proj, blk.mlp.fc1, blk.mlp.fc2):
+                        lin.forward = (lambda x, _l=lin: mx_ref.MXLinearFn.apply(x, _l.weight, _l.bias))
+                        n += 1
+            assert n == 32, n
+        logits = {}
+        m.classify.register_forward_hook(lambda mod, i, o: logits.__setitem__("z", o.detach().clone()))
+        m.train()
+        p = m((video, mel, wave))
+        loss = torch.nn.BCELoss()(p, label)
+        loss.backward()
+        grads.append({n: q.grad.clone() for n, q in m.named_parameters() if q.grad is not None})
+        outs.append((logits["z"], loss.detach()))
+    g32, g8 = grads
+    ef8 = {("ef8:" + n): _sampled_err(g8[n], g32[n], GC.GRAD_SAMPLE_C2) for n in g32 if n in g8}
+    zf = (outs[1][0].double() - outs[0][0].double()).abs().max() / outs[0][0].double().abs().max()
+    # relative L2 of all gradients together, over the tensors the parity test weighs (the analytically-zero
+    # ones excluded as tests/test_gpu_c2.GRAD_FLOOR does)
+    top = max(float(g.double().norm()) for g in g32.values())
+    num = den = 0.0
+    for n in g32:
+        if n in g8 and float(g32[n].double().norm()) >= 1e-6 * top:
+            num += float(((g8[n].double() - g32[n].double()) ** 2).sum())
+            den += float((g32[n].double() ** 2).sum())
+    l2 = (num / den) ** 0.5
+    print("ef8 median", sorted(ef8.values())[len(ef8) // 2], "max", max(ef8.values()), "logits", float(zf), "l2", l2)
+    save("fused_c2_fp8", z_train8=outs[1][0], loss8=outs[1][1], ef8_logits=zf, ef8_l2=l2, **ef8)
+
+
 def case_state_keys():
     """state_dict keys + shapes of the reference fused model at C1 and C2 (371 keys at C1)."""
     import json
@@ -414,6 +460,6 @@ if __name__ == "__main__":
     only = sys.argv[1:]
     for fn in [case_window_attention, case_block, case_patch_embed_merge, case_vst_c1, case_w2v, case_head,
                case_fused_c1, case_block_c2, case_mel_c2, case_fused_c1_grads, case_fused_c2, case_state_keys,
-               case_config_flags, case_inception, case_block_c4, case_pretrained]:
+               case_config_flags, case_inception, case_block_c4, case_pretrained, case_fused_c2_fp8]:
         if not only or fn.__name__ in only:
             fn()

@@ -40,3 +40,36 @@ def dequant(q, s):
     e = torch.stack([(dw >> (8 * j)) & 0xFF for j in range(4)], -1)     # [K/128, R, 4]
     e = e.permute(1, 0, 2).reshape(R, K // 32).float()
     return (v.reshape(R, K // 32, 32) * torch.pow(2.0, e - 127)[..., None]).reshape(R, K)
+
+
+def fq(x):
+    """Fake quantisation: x [R, K] (K % 128 == 0) through MX-fp8 and back (blocks of 32 along the last dim)."""
+    return dequant(*quant(x))
+
+
+class MXLinearFn(torch.autograd.Function):
+    """fp32 emulation of what set_fp8 does to one Linear (deepfake_amd/functional.py LinearFn / MlpFn, mx=True):
+    forward y = fq(x) fq(W)^T + b (MX blocks along the in-features), input gradient dx = fq(dy) fq(W^T)^T (blocks
+    along the out-features: the dX GEMM's contraction), weight / bias gradients from the unquantised x and dy (the
+    weight-gradient GEMMs stay bf16).  Used by make_golden.py to measure the error MX-fp8 alone costs the reference
+    model (the ``ef8:<param>`` anchors of tests/test_gpu_c4.py)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        x2 = x.reshape(-1, x.shape[-1])
+        y = fq(x2) @ fq(w).t()
+        if b is not None:
+            y = y + b
+        return y.reshape(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = (fq(dy2) @ fq(w.t().contiguous()).t()).reshape(x.shape)
+        dw = dy2.t() @ x2
+        db = dy2.sum(0) if ctx.has_b else None
+        return dx, dw, db

@@ -50,6 +50,14 @@ class Net(torch.nn.Module):
         return self.bn(self.b(h)).sum(-1)
 
 
+def _free_port():
+    """A TCP port free right now on 127.0.0.1 (fixed ports collide with sockets of an earlier test in TIME_WAIT)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 def _data(seed, n):
     g = torch.Generator().manual_seed(seed)
     return torch.randn(n, 16, generator=g), torch.randn(n, generator=g)
@@ -132,7 +140,8 @@ def test_accumulation_no_sync_matches_single_process_sum():
     step; non-final micro-steps launch no all-reduce (no_sync); BN statistics follow rank 0."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_accum_worker, args=(r, 2, 29513, q)) for r in range(2)]
+    port = _free_port()
+    procs = [ctx.Process(target=_accum_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, (torch.from_numpy(f), torch.from_numpy(rm), le)) for r, f, rm, le in (q.get(timeout=120) for _ in procs))
@@ -159,7 +168,7 @@ def test_accumulation_no_sync_matches_single_process_sum():
 def test_bucketed_allreduce_matches_global_batch(overlap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (7 if overlap else 9)
+    port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, overlap, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -212,7 +221,7 @@ def test_fused_model_bucket_layout(comm):
     dt = torch.bfloat16 if comm == "bf16" else torch.float32
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29521 if comm == "fp32" else 29523
+    port = _free_port()
     procs = [ctx.Process(target=_layout_worker, args=(r, 2, port, dt, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -270,7 +279,8 @@ def test_trainer_seeds_device_rng_per_rank():
     from deepfake_amd import rng
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_seed_worker, args=(r, 2, 29525, q)) for r in range(2)]
+    port = _free_port()
+    procs = [ctx.Process(target=_seed_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
     st = dict(q.get(timeout=120) for _ in procs)
@@ -324,7 +334,7 @@ def test_capture_failure_on_one_rank_moves_all_ranks(fail):
     form together and commit to the one-pass form (src/trainer.py:74-75 replaced by per-GPU DDP, §8e)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29531 if fail == "capture" else 29533
+    port = _free_port()
     procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, fail, q)) for r in range(2)]
     for p in procs:
         p.start()
@@ -346,7 +356,8 @@ def test_bf16_buckets_world4(world):
     from deepfake_amd.models.fused import build_fused
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_layout_worker, args=(r, world, 29541, torch.bfloat16, q)) for r in range(world)]
+    port = _free_port()
+    procs = [ctx.Process(target=_layout_worker, args=(r, world, port, torch.bfloat16, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict((r, g) for r, g, _, _ in (q.get(timeout=300) for _ in procs))
@@ -379,3 +390,78 @@ def test_watchdog_idle_raises_without_flight_recorder(monkeypatch):
         monkeypatch.delattr(c10d, n, raising=False)
     with pytest.raises(RuntimeError, match="flight-recorder"):
         ddp.watchdog_idle(timeout=0.1)
+
+
+def _finite_worker(rank, world, port, q):
+    from deepfake_amd.trainer import check_finite
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = []
+    for step, losses in ((1, (0.7, 0.69)), (2, (0.6, float("nan"))), (3, (float("inf"), 0.5))):
+        try:
+            check_finite(losses[rank], step, dist.group.WORLD)
+            res.append("ok")
+        except FloatingPointError as e:
+            res.append("raise:" + ("other" if "another rank" in str(e) else "own"))
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_check_finite_raises_on_every_rank():
+    """A non-finite loss on one rank makes EVERY rank raise at that log step (the flag is MAX-all-reduced), so the
+    healthy ranks do not block in the next gradient all-reduce until the RCCL watchdog fires."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_finite_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == ["ok", "raise:other", "raise:own"], res
+    assert res[1] == ["ok", "raise:own", "raise:other"], res
+
+
+def _fold_worker(rank, world, port, comm, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m = Net()
+    store = ParamStore(m, torch.float32, device=torch.device("cpu"))
+    bk = GradBucketer(store, bucket_mb=0.0002, comm_dtype=comm)
+    x, y = _data(1, 8)
+    xs, ys = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
+    ((m(xs) - ys) ** 2).mean().backward()
+    local = store.grad.clone()
+    fa = bk.finish(fold=True)
+    src = fa["grad_bf16"].float() if fa["grad_bf16"] is not None else store.grad
+    q.put((rank, local.numpy().copy(), src.numpy().copy(), fa["grad_scale"],
+           store.grad.numpy().copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("comm", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+def test_finish_fold_leaves_sum_and_scale(comm):
+    """finish(fold=True): no averaging pass — the all-reduced SUM stays where RCCL put it (the fp32 gradient
+    buffer, or the bf16 bucket copy while the fp32 buffer keeps the rank-local gradient) and the optimizer gets
+    grad_scale = 1 / world (FusedSGD folds both into its one pass over the parameters)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fold_worker, args=(r, 2, port, comm, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+    total = torch.from_numpy(res[0][0]) + torch.from_numpy(res[1][0])
+    for r in range(2):
+        local, src, scale, gbuf = (torch.from_numpy(v) if not isinstance(v, float) else v for v in res[r])
+        assert scale == 0.5
+        if comm == torch.float32:
+            assert torch.allclose(src, total, atol=1e-6)
+        else:
+            bound = 3 * 2 ** -8 * total.abs().max().item()
+            assert (src - total).abs().max().item() <= bound
+            assert torch.equal(gbuf, local)        # the fp32 buffer is not overwritten with the sum

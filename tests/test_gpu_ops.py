@@ -225,6 +225,34 @@ def test_cpb_bias_and_cosine_logit_scale(heads, clamped):
     assert rel(logit.grad, lr.grad) < 1e-4
 
 
+def test_cpb_tables_batched():
+    """Every SwinV2 block's CPB table in one launch each way (Fn.cpb_tables, dfk_cpb_bias_*_many): forward tables
+    and every parameter gradient equal the per-block kernels' (same arithmetic per table), over blocks of
+    different head counts and window sizes — including a block whose table gets no gradient."""
+    from deepfake_amd import functional as Fn
+    from deepfake_amd.models.swin_transformer2d import WindowAttention
+    torch.manual_seed(5)
+    attns = [WindowAttention(64, (7, 7), 4, pretrained_window_size=(16, 16)),
+             WindowAttention(128, (7, 7), 8), WindowAttention(512, (5, 5), 16),
+             WindowAttention(1024, (7, 7), 32, pretrained_window_size=(16, 16))]
+    attns = [a.to(DEV) for a in attns]
+    tabs = Fn.cpb_tables(attns)
+    douts = [torch.randn_like(t) for t in tabs]
+    sum((t * d).sum() for t, d in zip(tabs[:3], douts[:3])).backward()   # the 4th table: no gradient
+    got = [[p.grad.clone() if p.grad is not None else torch.zeros_like(p)
+            for p in (a.cpb_mlp[0].weight, a.cpb_mlp[0].bias, a.cpb_mlp[2].weight)] for a in attns]
+    for a in attns:
+        a.zero_grad(set_to_none=True)
+    for i, a in enumerate(attns):
+        t = a.bias_table()
+        assert rel(tabs[i], t) < 1e-6, i
+        if i < 3:
+            (t * douts[i]).sum().backward()
+        for gp, p in zip(got[i], (a.cpb_mlp[0].weight, a.cpb_mlp[0].bias, a.cpb_mlp[2].weight)):
+            ref = p.grad if p.grad is not None else torch.zeros_like(p)
+            assert rel(gp, ref) < 1e-5 if i < 3 else float(gp.abs().max()) == 0.0, i
+
+
 @pytest.mark.parametrize("C", [96, 384])
 def test_skip_gradient_fusion(C):
     """Skip forms of LayerNormFn / MlpFn (one backward pass adds the gradient the input receives along the

@@ -208,6 +208,33 @@ def test_layerdrop_flags_and_sgd_gate():
     assert rel(p, p0 - 0.1 * (gr + 0.05 * p0)) < 1e-6
 
 
+@pytest.mark.parametrize("world", [3, 4])
+def test_sgd_data_parallel_fold(world):
+    """The fused step consumes the all-reduced SUM: grad_scale = 1 / world replaces the averaging pass, and
+    grad_bf16 reads the bf16 bucket copy in place of the fp32 buffer (ddp.GradBucketer.finish(fold=True)).
+    Odd lengths cover the scalar tail."""
+    for n in (1000, 1003):
+        g = torch.Generator(device=DEV).manual_seed(n)
+        p0 = torch.randn(n, device=DEV, generator=g)
+        gsum = torch.randn(n, device=DEV, generator=g) * world
+        for first in (True, False):
+            b0 = torch.randn(n, device=DEV, generator=g)
+            # fp32 sum in the gradient buffer
+            p, buf = p0.clone(), b0.clone()
+            K.sgd_step(p, gsum, buf, None, 0.1, 0.9, 0.05, first, grad_scale=1.0 / world)
+            gm = gsum * (1.0 / world) + 0.05 * p0
+            bref = gm if first else 0.9 * b0 + gm
+            assert rel(buf, bref) < 1e-6 and rel(p, p0 - 0.1 * bref) < 1e-6
+            # bf16 sum in the bucket copy (the fp32 buffer holds something else and must not be read)
+            gb = gsum.to(torch.bfloat16)
+            p, buf = p0.clone(), b0.clone()
+            K.sgd_step(p, torch.full_like(gsum, float("nan")), buf, None, 0.1, 0.9, 0.05, first,
+                       grad_scale=1.0 / world, grad_bf16=gb)
+            gm = gb.float() * (1.0 / world) + 0.05 * p0
+            bref = gm if first else 0.9 * b0 + gm
+            assert rel(buf, bref) < 1e-6 and rel(p, p0 - 0.1 * bref) < 1e-6
+
+
 def test_fused_c1_regularized_step():
     """The C1 fused model with the reference's regularisers trains (finite loss, gradients everywhere the
     reference has them), its masks change from step to step, and eval mode is the deterministic model."""
