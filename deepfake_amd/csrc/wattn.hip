@@ -1225,6 +1225,9 @@ __global__ __launch_bounds__(256, (HD == 32 && !DROP) ? 3 : 2) void wattn_fwd4_k
 constexpr int kF5Slots = 13;   // per wave and lane: 8 float4 of pair partials, 4 of tail partials, 1 of l's
 
 __device__ __forceinline__ bool f5_l_ok(float l) {   // bit test: NaN-proof under this file's no-NaN flags
+#ifdef DFK5_ABL   // ablation builds (tools/exp_build.sh): never take the fallback
+  return true;
+#endif
   const uint32_t u = __float_as_uint(l);
   return u >= 0x17800000u && u <= 0x71800000u;          // 2^-80 <= l <= 2^100, positive, finite
 }
