@@ -89,8 +89,8 @@ def time_kernel(fn, iters):
     return s.elapsed_time(e) / iters * 1e-3   # seconds per launch
 
 
-ROOFLINE_KERNEL = "wattn_fwd4_kernel<32, false, 2>"
-ROOFLINE_PMC = os.path.join(HERE, "profiles", "r4", "r4z_wattn_fwd_pmc.json")   # tools/gpu_round4.sh r4z
+ROOFLINE_KERNEL = "wattn_fwd6_kernel<false>"
+ROOFLINE_PMC = os.path.join(HERE, "profiles", "r5", "r5_wattn_fwd_pmc.json")   # tools/roofline_pmc.sh (round 5)
 
 
 def stage1_geometry(cfg):
@@ -122,7 +122,7 @@ def roofline_case(cfg, B, dt):
     out = torch.empty(rows, C, device="cuda", dtype=dt)
     args = (qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, (B, D, H, W), win, win, shift, heads, hd, hd ** -0.5)
     # the bf16 score-bias tiles (dfk_wattn_table, a separate launch) are built once: the timed launch is the
-    # attention kernel alone, the one rocprofv3 lists as wattn_fwd4_kernel<32, false, 2>
+    # attention kernel alone, the one rocprofv3 lists as wattn_fwd6_kernel<false> (16x16x32 tiles)
     _, _, tab = K.wattn_fwd(*args, rpb=rpb, out=out, return_table=True)
 
     def run():
@@ -146,7 +146,7 @@ def pmc_traffic():
 
 
 CONV3D_KERNEL = "pe_fwd_kernel<6>"
-CONV3D_INSTEP = os.path.join(HERE, "profiles", "r4", "r4z_conv3d_instep.json")   # tools/gpu_round4.sh r4z
+CONV3D_INSTEP = os.path.join(HERE, "profiles", "r5", "r5_conv3d_instep.json")   # tools/gpu_round5.sh
 
 
 def conv3d_in_step():
@@ -191,6 +191,45 @@ def conv3d_roofline(cfg, B, iters, nbuf=3, instep=False):
             "in_step": conv3d_in_step() if instep else None}
 
 
+ATTN_BWD_KERNELS = "wattn_bwd3_kernel<32, true, false> + drpb_from_ds_kernel + drpb_reduce_kernel"
+
+
+def attn_bwd_roofline(cfg, B, dt, iters):
+    """The stage-1 shifted-window attention BACKWARD of the same launch as `roofline` (WindowAttention3D.forward's
+    autograd, video_swin_transformer.py:142-173): dQ, dK, dV and the relative-position-bias gradient dRPB, i.e.
+    the backward kernel plus the two dRPB launches (binning the dS scratch, reducing the partial rows).
+    Algorithmic FLOPs = 10 * window-heads * N^2 * hd (dP = dO V^T, dV = P^T dO, dS -> dQ = dS K, dK = dS^T Q, plus the
+    recomputed S = Q K^T); the dRPB binning is counted as no FLOPs."""
+    from deepfake_amd import kernels as K
+    C, heads, win, shift, (D, H, W) = stage1_geometry(cfg)
+    hd = C // heads
+    rows = B * D * H * W
+    g = torch.Generator(device="cuda").manual_seed(8)
+    qkv = torch.randn(rows, 3 * C, device="cuda", generator=g).to(dt)
+    nW = -(-D // win[0]) * -(-H // win[1]) * -(-W // win[2])
+    N = win[0] * win[1] * win[2]
+    L = (2 * win[0] - 1) * (2 * win[1] - 1) * (2 * win[2] - 1)
+    rpb = torch.randn(L, heads, device="cuda", generator=g) * 0.02
+    args = (qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, (B, D, H, W), win, win, shift, heads, hd, hd ** -0.5)
+    out, lse, tab = K.wattn_fwd(*args, rpb=rpb, return_table=True)
+    dout = torch.randn(rows, C, device="cuda", generator=g).to(dt)
+    dqkv = torch.empty_like(qkv)
+    drpb = torch.zeros_like(rpb)
+    fa = (qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, 3 * C, (B, D, H, W), win, win, shift, heads, hd, hd ** -0.5,
+          rpb, None)
+
+    def run():
+        K.wattn_bwd(fa, dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C, drpb=drpb, tab=tab)
+    t = time_kernel(run, iters)
+    flops = 10.0 * B * nW * heads * N * N * hd
+    ach = flops / t / 1e12
+    return {"kernel": ATTN_BWD_KERNELS + f" (stage-1 SW-MSA backward with dRPB, {N}-token windows, {heads} heads x "
+            f"{hd}, {B * nW * heads} window-heads)", "bound": "mfma", "achieved": round(ach, 2),
+            "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+            "flops_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4),
+            "timing": f"HIP events over {iters} calls of the three launches"}
+
+
 def roofline(cfg, B, dt, iters, pmc=True):
     run, flops, desc = roofline_case(cfg, B, dt)
     t = time_kernel(run, iters)
@@ -203,6 +242,22 @@ def roofline(cfg, B, dt, iters, pmc=True):
 
 
 GEMM_KERNEL = "gemm_dma_kernel<32|64, N, N, 2>"
+
+
+def gemm_bound(flops, nbytes, t, peak_tflops):
+    """Label a GEMM launch by its arithmetic intensity against the ridge of its dtype (peak FLOP/s over the 8 TB/s
+    HBM peak): below the ridge it is HBM-bound and its fraction is bytes / time over HBM peak, above it MFMA-bound."""
+    ridge = peak_tflops * 1e12 / (PEAK_HBM_GBS * 1e9)
+    intensity = flops / nbytes
+    if intensity < ridge:
+        ach = nbytes / t / 1e9
+        return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(ach / PEAK_HBM_GBS, 4), "tflops": round(flops / t / 1e12, 2),
+                "intensity_flop_per_byte": round(intensity, 1), "ridge_flop_per_byte": round(ridge, 1)}
+    ach = flops / t / 1e12
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tflops, "unit": "TFLOP/s",
+            "frac": round(ach / peak_tflops, 4), "intensity_flop_per_byte": round(intensity, 1),
+            "ridge_flop_per_byte": round(ridge, 1)}
 
 
 PEAK_FP8_TFLOPS = 5000.0       # MI355X dense fp8 (block-scaled MX e4m3) MFMA (MI355X_MICROARCH.md)
@@ -233,22 +288,19 @@ def gemm_roofline(cfg, B, iters, fp8=False):
         def run_mx():
             K.gemm_mx(xq, wq, bias=b, out=out, act=1, aux=aux, mx_out=True)
         t = time_kernel(run_mx, iters)
-        achieved = flops / t / 1e12
-        return {"kernel": MX_GEMM_KERNEL + f" ({trunk} stage-3 Mlp.fc1 fwd on MX-fp8, [{M},{Kd}]x[{Kd},{N}] + bias + "
-                "GELU, pre-activation saved, h also written quantised for fc2)",
-                "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP8_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP8_TFLOPS, 4), "flops_per_launch": flops,
-                "bytes_per_launch": M * Kd * (1 + 1 / 32) + N * Kd * (1 + 1 / 32) + M * N * (2 + 2 + 1 + 1 / 32),
-                "avg_launch_ms": round(t * 1e3, 4)}
+        nbytes = M * Kd * (1 + 1 / 32) + N * Kd * (1 + 1 / 32) + M * N * (2 + 2 + 1 + 1 / 32)
+        return dict({"kernel": MX_GEMM_KERNEL + f" ({trunk} stage-3 Mlp.fc1 fwd on MX-fp8, [{M},{Kd}]x[{Kd},{N}] + "
+                     "bias + GELU, pre-activation saved, h also written quantised for fc2)"},
+                    **gemm_bound(flops, nbytes, t, PEAK_FP8_TFLOPS), flops_per_launch=flops,
+                    bytes_per_launch=round(nbytes), avg_launch_ms=round(t * 1e3, 4))
 
     def run():
         K.linear(x, w, b, out=out, act=1, aux=aux)
     t = time_kernel(run, iters)
-    achieved = flops / t / 1e12
-    return {"kernel": GEMM_KERNEL + f" ({trunk} stage-3 Mlp.fc1 fwd, [{M},{Kd}]x[{Kd},{N}] + bias + GELU, pre-activation saved)",
-            "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "flops_per_launch": flops,
-            "bytes_per_launch": (M * Kd + 2 * M * N + N * Kd) * 2, "avg_launch_ms": round(t * 1e3, 4)}
+    nbytes = (M * Kd + 2 * M * N + N * Kd) * 2
+    return dict({"kernel": GEMM_KERNEL + f" ({trunk} stage-3 Mlp.fc1 fwd, [{M},{Kd}]x[{Kd},{N}] + bias + GELU, "
+                 "pre-activation saved)"}, **gemm_bound(flops, nbytes, t, PEAK_BF16_TFLOPS), flops_per_launch=flops,
+                bytes_per_launch=nbytes, avg_launch_ms=round(t * 1e3, 4))
 
 
 DW_KERNEL = "gemm_dma_kernel<64, 2, 2, true, true, 2, true, false>"
@@ -413,6 +465,7 @@ def main():
     roof_conv = conv3d_roofline(cfg, a.batch, a.roofline_iters, instep=c2) if rank == 0 else None
     roof_gemm = gemm_roofline(cfg, a.batch, a.roofline_iters, fp8=a.dtype == "fp8") if rank == 0 else None
     roof_dw = dw_roofline(cfg, a.batch, a.roofline_iters) if rank == 0 else None
+    roof_bwd = attn_bwd_roofline(cfg, a.batch, dt, a.roofline_iters) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
@@ -432,7 +485,8 @@ def main():
                        "branch_streams": 3,
                        "regularisers": not a.deterministic, "loss": round(lossv, 5)},
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2) if train_gflop else None,
-            "roofline": roof, "roofline_conv3d": roof_conv, "roofline_gemm": roof_gemm, "roofline_dw": roof_dw,
+            "roofline": roof, "roofline_attn_bwd": roof_bwd, "roofline_conv3d": roof_conv, "roofline_gemm": roof_gemm,
+            "roofline_dw": roof_dw,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -666,18 +666,20 @@ __device__ __forceinline__ float grp_max4(float v) {
 // Score bias in log2 units, bf16, in the operand order of the MFMA that adds it:
 //   bias'(q, k) = (rpb[pos(q) - pos(k) + C0] + (label(q) != label(k) ? -100 : 0)) * log2(e),
 //   -1e4 for keys >= N (finite: the identity product below must never meet an infinity), 0 for queries >= N.
-// The tile streams as 2 KB of bf16 (4 KB as fp32).  The forward adds it through the C input of the first QK^T
-// MFMA (unpacked to fp32 on the VALU, with -m folded in), so its layout is the S^T accumulator's; the backward
-// adds it with two v_mfma_f32_32x32x16_bf16 products bias_c x I_c (I_c[slot][n] = (slot == n - 16c), a constant
-// identity operand), so its layout is that product's A operand:
-//   fwd layout (S^T accumulator: key on the row, query on the lane) [cls][head][qb][kb][c][64 lanes][8]:
+// The tile streams as 2 KB of bf16 (4 KB as fp32).  Forward and backward add it through the C input of the score
+// MFMA (unpacked to fp32 on the VALU), so each layout is that accumulator's:
+//   fwd layout (v4 / v5, S^T 32x32 accumulator: key on the row, query on the lane) [cls][head][qb][kb][c][64][8]:
 //       lane l, element jj, j = 8 c + jj <-> q = 32 qb + (l & 31), k = 32 kb + (j & 3) + 8 (j >> 2) + 4 (l >> 5)
-//   bwd layout (S: query on the row, key on the lane)  [cls][head][qb][kb][c][64 lanes][8]:
-//       lane l, element j <-> q = 32 qb + (l & 31), k = 32 kb + 16 c + 8 (l >> 5) + j
+//   fwd16 layout (v6, four 16x16 S^T sub-tiles, dfk_wattn_fwd_policy version 6): same tile size and order,
+//       lane l, element j of c <-> q = 32 qb + 16 c + (l & 15), k = 32 kb + 16 (j >> 2) + 4 (l >> 4) + (j & 3)
+//   bwd layout (S 32x32 accumulator: query on the row, key on the lane) [cls][head][qb][kb][c][64 lanes][8]:
+//       lane l, element jj, j = 8 c + jj <-> q = 32 qb + 8 (j >> 2) + 4 (l >> 5) + (j & 3), k = 32 kb + (l & 31)
+//       (r5: through the C input with -L'; it was two identity-operand MFMAs, which the mel windows paid
+//        for: mel1 backward 30 -> 25 us, the 392-token windows unchanged)
 constexpr float kPadKey = -1.0e4f;
 
 __global__ __launch_bounds__(256) void wattn_tab3_kernel(const dfk_wattn_args a, const Geo g, bf16raw* __restrict__ tf,
-                                                         bf16raw* __restrict__ tb) {
+                                                         bf16raw* __restrict__ tb, int fwd16) {
   extern __shared__ int tsm[];
   int* tok = tsm;                                          // [Np]
   float* rp = reinterpret_cast<float*>(tsm + g.Np);        // [L]
@@ -708,13 +710,18 @@ __global__ __launch_bounds__(256) void wattn_tab3_kernel(const dfk_wattn_args a,
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
       float v0, v1;
-      if (!bwd) {
+      if (!bwd && fwd16) {   // v6 (16x16x32 tiles): lane l, c = query half, j = 4 kh + r
+        const int qq = qb * 32 + 16 * c + (lane & 15), kq = kb * 32 + 4 * (lane >> 4);
+        v0 = val(qq, kq + 16 * (j >> 2) + (j & 3));
+        v1 = val(qq, kq + 16 * ((j + 1) >> 2) + ((j + 1) & 3));
+      } else if (!bwd) {
         const int j0 = 8 * c + j, j1 = j0 + 1;
         v0 = val(qb * 32 + rr, kb * 32 + (j0 & 3) + 8 * (j0 >> 2) + 4 * hh);
         v1 = val(qb * 32 + rr, kb * 32 + (j1 & 3) + 8 * (j1 >> 2) + 4 * hh);
       } else {
-        v0 = val(qb * 32 + rr, kb * 32 + 16 * c + 8 * hh + j);
-        v1 = val(qb * 32 + rr, kb * 32 + 16 * c + 8 * hh + j + 1);
+        const int j0 = 8 * c + j, j1 = j0 + 1;   // the C-input layout of the backward's S (key on the lane)
+        v0 = val(qb * 32 + 8 * (j0 >> 2) + 4 * hh + (j0 & 3), kb * 32 + rr);
+        v1 = val(qb * 32 + 8 * (j1 >> 2) + 4 * hh + (j1 & 3), kb * 32 + rr);
       }
       pw[j >> 1] = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
     }
@@ -1583,6 +1590,365 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd5_kernel(const dfk_wattn_args
   }
 }
 
+// sum over the 4 lane groups (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float grp_sum4(float v) {
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float s = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+}
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Forward v6 (hd 32, bias tables, no dropout; experiment, DFK_WATTN_V=6): v5 on v_mfma_f32_16x16x32_bf16.  With
+// K = hd = 32 one 16x16x32 product is a whole 16x16 score sub-tile: the four sub-tiles of a 32x32 block are four
+// independent MFMAs with no accumulate chain, and each sub-tile's v_exp can start as soon as its own product is
+// done (v5's 32x32x16 tile waits on two dependent products before its first v_exp; r5e ablation: that wait is
+// ~50 us of the stage-1 launch).  Lane l holds, per chain and query half qh, query 32 qb + 16 qh + (l & 15) and keys
+// 16 kh + 4 (l >> 4) + r of each key half kh; the P^T operand of the PV product is the lane's own 8 scores
+// (k-slots j <-> key 16 (j >> 2) + 4 (l >> 4) + (j & 3)), and V^T is read with the same slot order by ds_read_tr16.
+// Row statistics are per (chain, half) and reduce over the 4 lane groups.  Bias tables in the fwd16 layout
+// (wattn_tab3_kernel fwd16: [qh][64 lanes][kh][r]).
+template <bool BAL>
+__global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args a, const Geo g, int qsplit,
+                                                           const bf16raw* __restrict__ tab) {
+  constexpr int HD = 32, CH = HD / 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16raw* Ks = reinterpret_cast<bf16raw*>(smem);
+  bf16raw* Vs = Ks + (size_t)g.Np * HD;
+  const int tid = dfk_tid(), lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ql = lane & 15, g16 = lane >> 4, tq = ql >> 2, tp = ql & 3;
+  const WUnit wu = decode_unit(a, g, qsplit);
+  const int head = wu.head, win = wu.win, b = wu.b;
+  const long unit = wu.lse_unit;
+  const int hoff = head * HD;
+  auto gather = [&]() __attribute__((always_inline)) {   // K / V of the window -> swizzled LDS tiles (as v5)
+    constexpr int KV_B = 4;
+    const int tot = g.Np * CH;
+    for (int base = tid; base < tot; base += KV_B * dfk_bdim()) {
+      uint4 kv[KV_B], vv[KV_B];
+      int off[KV_B];
+#pragma unroll
+      for (int u = 0; u < KV_B; ++u) {
+        const int idx = min(base + u * (int)dfk_bdim(), tot - 1);
+        const int i = idx / CH, c = (idx % CH) * 8;
+        const int row = token_info_row(a, g, b, win, i);
+        off[u] = swz<HD>(i, c);
+        kv[u] = tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + c);
+        vv[u] = tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + c);
+      }
+#pragma unroll
+      for (int u = 0; u < KV_B; ++u) {
+        if (base + u * (int)dfk_bdim() < tot) {
+          *reinterpret_cast<uint4*>(Ks + off[u]) = kv[u];
+          *reinterpret_cast<uint4*>(Vs + off[u]) = vv[u];
+        }
+      }
+    }
+  };
+  gather();
+  const int nkb = g.Np / 32, nqb = nkb;
+  const bf16raw* tch = tab + ((long)wu.cls * a.heads + head) * (long)g.Np * g.Np;
+  const float qs = a.scale * kLog2e;
+  int koff[2], vlo[2], vhi[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    koff[h] = swz<HD>(16 * h + ql, 8 * g16);
+    vlo[h] = swz<HD>(4 * g16 + tq, 16 * h + 4 * tp);
+    vhi[h] = swz<HD>(16 + 4 * g16 + tq, 16 * h + 4 * tp);
+  }
+  const uint64_t tp64 = reinterpret_cast<uint64_t>(tch);
+  const uint64_t tpu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(tp64 >> 32)) << 32) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)tp64);
+  const __amdgpu_buffer_rsrc_t trs =
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(tpu), (short)0, 0x7fffffff, 0x00020000);
+  __syncthreads();
+
+  // scaled Q fragments of query block qb: half qh = B operand of the 16x16x32 products (query 32 qb + 16 qh + ql,
+  // channels 8 g16 .. 8 g16 + 7)
+  auto load_q = [&](int qb, bf16x8 (&qf)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const int q = qb * 32 + 16 * qh + ql;
+      const int row = q < g.N ? token_info_row(a, g, b, win, q) : -2;
+      const bf16x8 raw = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.q, a.pad_q, row, a.ld_qkv, hoff + 8 * g16));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[qh][j] = (__bf16)((float)raw[j] * qs);
+    }
+  };
+  // element index in a chain's 16 registers: scores d[8 qh + 4 kh + r], output o[8 qh + 4 eh + r]
+  auto chains = [&](auto nc_t, auto safe_t, const int (&qb)[2], const bf16x8 (&qf)[2][2], int k0, int k1,
+                    f32x16 (&o)[2], float (&ls)[2][2], float (&m)[2][2]) __attribute__((always_inline)) {
+    constexpr int NC = decltype(nc_t)::value;
+    constexpr bool SAFE = decltype(safe_t)::value;
+    auto load_bias = [&](uint4 (&bt)[2][2], int kb) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < NC; ++u) {
+        const int so = __builtin_amdgcn_readfirstlane((qb[u] * nkb + kb) * 2048);
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          bt[u][c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(trs, lane * 16, so + c * 1024, 0));
+      }
+    };
+    uint4 bt[2][2];
+    load_bias(bt, k0);
+    for (int kb = k0; kb < k1; ++kb) {
+      const bf16raw* kbase = Ks + kb * 32 * HD;
+      const bf16raw* vbase = Vs + kb * 32 * HD;
+      bf16x8 kf[2];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) kf[kh] = *reinterpret_cast<const bf16x8*>(kbase + koff[kh]);
+      f32x4 d[2][4];
+#pragma unroll
+      for (int u = 0; u < NC; ++u)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const uint32_t w[4] = {bt[u][c].x, bt[u][c].y, bt[u][c].z, bt[u][c].w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xffff0000u);
+            if constexpr (SAFE) {
+              lo -= m[u][c];
+              hi -= m[u][c];
+            }
+            d[u][2 * c + (i >> 1)][2 * (i & 1)] = lo;
+            d[u][2 * c + (i >> 1)][2 * (i & 1) + 1] = hi;
+          }
+        }
+      load_bias(bt, min(kb + 1, k1 - 1));
+#pragma unroll
+      for (int u = 0; u < NC; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) d[u][t] = mfma16(kf[t & 1], qf[u][t >> 1], d[u][t]);
+      bf16x8 va[2];
+#pragma unroll
+      for (int eh = 0; eh < 2; ++eh) va[eh] = tr16x2(vbase + vlo[eh], vbase + vhi[eh]);
+#pragma unroll
+      for (int u = 0; u < NC; ++u) {
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          f32x4& d0 = d[u][2 * qh];
+          f32x4& d1 = d[u][2 * qh + 1];
+          if constexpr (SAFE) {
+            float bm = max3f(max3f(d0[0], d0[1], d0[2]), max3f(d0[3], d1[0], d1[1]), max3f(d1[2], d1[3], -INFINITY));
+            bm = grp_max4(bm);
+            const bool grow = kb == k0 || bm > kRescale;
+            if (__builtin_amdgcn_ballot_w64(grow) != 0) {
+              const float mn = grow ? bf16_ceil(m[u][qh] + bm) : m[u][qh];
+              const float delta = mn - m[u][qh];
+              const float alpha = kb == k0 ? 0.f : __builtin_amdgcn_exp2f(-delta);
+              m[u][qh] = mn;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                d0[j] -= delta;
+                d1[j] -= delta;
+              }
+              ls[u][qh] *= alpha;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) o[u][8 * qh + j] *= alpha;
+            }
+          }
+          float p[8];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            p[j] = __builtin_amdgcn_exp2f(d0[j]);
+            p[4 + j] = __builtin_amdgcn_exp2f(d1[j]);
+          }
+          ls[u][qh] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+          bf16x8 pv;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pv[j] = (__bf16)p[j];
+#pragma unroll
+          for (int eh = 0; eh < 2; ++eh) {
+            f32x4 acc = {o[u][8 * qh + 4 * eh], o[u][8 * qh + 4 * eh + 1], o[u][8 * qh + 4 * eh + 2],
+                         o[u][8 * qh + 4 * eh + 3]};
+            acc = mfma16(va[eh], pv, acc);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[u][8 * qh + 4 * eh + j] = acc[j];
+          }
+        }
+      }
+    }
+  };
+  auto zero = [&](f32x16 (&o)[2], float (&ls)[2][2], float (&m)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) ls[u][qh] = m[u][qh] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) o[u][j] = 0.f;
+    }
+  };
+  // O = O^T / l for block qb (lane: queries 32 qb + 16 qh + ql, channels 16 eh + 4 g16 + 0..3), lse; true: rejected
+  auto store = [&](int qb, const f32x16& o, const float (&ls)[2], const float (&m)[2], bool real = true,
+                   bool reduced = false) __attribute__((always_inline)) -> bool {
+    if (!real) return false;
+    bool bad = false;
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh) {
+      const float l = reduced ? ls[qh] : grp_sum4(ls[qh]);
+      const float inv = 1.f / l;
+      const int q = qb * 32 + 16 * qh + ql;
+      const int row = q < g.N ? token_info_row(a, g, b, win, q) : -2;
+      if (row >= 0) {
+        bf16raw* op = reinterpret_cast<bf16raw*>(a.out) + (long)row * a.ld_out + hoff + 4 * g16;
+#pragma unroll
+        for (int eh = 0; eh < 2; ++eh) {
+          uint2 w;
+          w.x = (uint32_t)f2bf(o[8 * qh + 4 * eh] * inv) | ((uint32_t)f2bf(o[8 * qh + 4 * eh + 1] * inv) << 16);
+          w.y = (uint32_t)f2bf(o[8 * qh + 4 * eh + 2] * inv) | ((uint32_t)f2bf(o[8 * qh + 4 * eh + 3] * inv) << 16);
+          *reinterpret_cast<uint2*>(op + 16 * eh) = w;
+        }
+      }
+      if (a.lse && g16 == 0 && q < g.N) a.lse[unit * g.Np + q] = (m[qh] + __log2f(l)) * 0.6931471805599453f;
+      bad |= !f5_l_ok(l);
+    }
+    return bad;
+  };
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using FAST = std::false_type;
+  using SAFE = std::true_type;
+  auto safe_block = [&](int qb) __attribute__((always_inline)) {
+    const int qbs[2] = {qb, qb};
+    bf16x8 qf[2][2];
+    load_q(qb, qf[0]);
+    f32x16 o[2];
+    float ls[2][2], m[2][2];
+    zero(o, ls, m);
+    chains(I1{}, SAFE{}, qbs, qf, 0, nkb, o, ls, m);
+    store(qb, o[0], ls[0], m[0]);
+  };
+  auto full = [&](int qb0, int qb1) __attribute__((always_inline)) {
+    const int qb[2] = {qb0, min(qb1, nqb - 1)};
+    bf16x8 qf[2][2];
+    load_q(qb[0], qf[0]);
+    load_q(qb[1], qf[1]);
+    f32x16 o[2];
+    float ls[2][2], m[2][2];
+    zero(o, ls, m);
+    chains(I2{}, FAST{}, qb, qf, 0, nkb, o, ls, m);
+    bool bad = store(qb[0], o[0], ls[0], m[0]);
+    bad |= store(qb[1], o[1], ls[1], m[1], qb1 < nqb);
+    if (__builtin_amdgcn_ballot_w64(bad) != 0) {
+      safe_block(qb[0]);
+      if (qb1 < nqb) safe_block(qb1);
+    }
+  };
+  const int nw = dfk_bdim() >> 6;
+  if constexpr (!BAL) {
+    const int ngrp = (nqb + 1) / 2, qstep = nw * qsplit;
+    for (int gi = wu.qpart * nw + wave; gi < ngrp; gi += qstep) full(2 * gi, 2 * gi + 1);
+    return;
+  } else {
+    // v5's balanced schedule (host guarantees: qsplit == 1, 4 waves, pairs % 4 in {0, 1, 2}); the row sums are
+    // reduced over the lane groups before they go to LDS, so the l's of a wave fit one float4 slot per lane
+    int& f5_flag = *reinterpret_cast<int*>(smem + max(4 * g.Np * HD, 4 * kF5Slots * 1024));
+    if (tid == 0) f5_flag = 0;
+    const int pairs = nqb / 2, tail = nqb & 1, R = pairs % 4, p1 = pairs - R;
+    for (int p = wave; p < p1; p += 4) full(2 * p, 2 * p + 1);
+    f32x16 oa[2], ob[2];
+    float la[2][2], lb[2][2], ma[2][2], mb[2][2];
+    zero(oa, la, ma);
+    zero(ob, lb, mb);
+    const int pa = R == 2 ? p1 + (wave >> 1) : p1;
+    if (R > 0) {
+      const int ka0 = R == 2 ? ((wave & 1) ? (nkb + 1) / 2 : 0) : (wave * nkb) / 4;
+      const int ka1 = R == 2 ? ((wave & 1) ? nkb : (nkb + 1) / 2) : ((wave + 1) * nkb) / 4;
+      const int qb[2] = {2 * pa, 2 * pa + 1};
+      bf16x8 qf[2][2];
+      load_q(qb[0], qf[0]);
+      load_q(qb[1], qf[1]);
+      chains(I2{}, FAST{}, qb, qf, ka0, ka1, oa, la, ma);
+    }
+    if (tail) {
+      const int qb[2] = {nqb - 1, nqb - 1};
+      bf16x8 qf[2][2];
+      load_q(qb[0], qf[0]);
+      chains(I1{}, FAST{}, qb, qf, (wave * nkb) / 4, ((wave + 1) * nkb) / 4, ob, lb, mb);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        la[u][qh] = grp_sum4(la[u][qh]);
+        lb[u][qh] = grp_sum4(lb[u][qh]);
+      }
+    __syncthreads();   // every wave is done with K / V: their space takes the partials
+    float4* ps = reinterpret_cast<float4*>(smem);
+    auto slot = [&](int w, int s) __attribute__((always_inline)) -> float4* { return ps + (w * kF5Slots + s) * 64 + lane; };
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4)
+        *slot(wave, 4 * u + j4) = make_float4(oa[u][4 * j4], oa[u][4 * j4 + 1], oa[u][4 * j4 + 2], oa[u][4 * j4 + 3]);
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4)
+      *slot(wave, 8 + j4) = make_float4(ob[0][4 * j4], ob[0][4 * j4 + 1], ob[0][4 * j4 + 2], ob[0][4 * j4 + 3]);
+    // slot 12: lanes of group 0 hold the pair's (chain, half) sums, group 1 the tail's (query = lane & 15)
+    *slot(wave, 12) = g16 == 0 ? make_float4(la[0][0], la[0][1], la[1][0], la[1][1])
+                               : make_float4(lb[0][0], lb[0][1], 0.f, 0.f);
+    __syncthreads();
+    const bool fin_pair = R == 2 ? (wave == 0 || wave == 2) : (R == 1 && wave == 0);
+    const bool fin_tail = tail && wave == (R == 2 ? 3 : (R == 1 ? 1 : 0));
+    bool bad2 = false;
+    if (fin_pair) {
+      const int w0 = R == 2 ? wave : 0, w1 = R == 2 ? wave + 2 : 4;
+      f32x16 o[2];
+      float ls[2][2], m0[2] = {0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        ls[u][0] = ls[u][1] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) o[u][j] = 0.f;
+      }
+      for (int w = w0; w < w1; ++w) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int j4 = 0; j4 < 4; ++j4) {
+            const float4 v = *slot(w, 4 * u + j4);
+            o[u][4 * j4] += v.x; o[u][4 * j4 + 1] += v.y; o[u][4 * j4 + 2] += v.z; o[u][4 * j4 + 3] += v.w;
+          }
+        const float4 lv = ps[(w * kF5Slots + 12) * 64 + ql];
+        ls[0][0] += lv.x; ls[0][1] += lv.y; ls[1][0] += lv.z; ls[1][1] += lv.w;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) bad2 |= store(2 * pa + u, o[u], ls[u], m0, true, true);
+    }
+    if (fin_tail) {
+      f32x16 o;
+      float ls[2] = {0.f, 0.f}, m0[2] = {0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) o[j] = 0.f;
+      for (int w = 0; w < 4; ++w) {
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const float4 v = *slot(w, 8 + j4);
+          o[4 * j4] += v.x; o[4 * j4 + 1] += v.y; o[4 * j4 + 2] += v.z; o[4 * j4 + 3] += v.w;
+        }
+        const float4 lv = ps[(w * kF5Slots + 12) * 64 + 16 + ql];
+        ls[0] += lv.x;
+        ls[1] += lv.y;
+      }
+      bad2 |= store(nqb - 1, o, ls, m0, true, true);
+    }
+    const bool wave_bad = __builtin_amdgcn_ballot_w64(bad2) != 0;   // every lane votes (not under lane == 0)
+    if (lane == 0 && wave_bad) f5_flag = 1;
+    __syncthreads();
+    if (f5_flag) {   // a rejected split block (vanishingly rare): K / V again, the block through the SAFE loop
+      gather();
+      __syncthreads();
+      if (__builtin_amdgcn_ballot_w64(bad2) != 0) {
+        safe_block(fin_pair ? 2 * pa : nqb - 1);
+        if (fin_pair) safe_block(2 * pa + 1);
+      }
+    }
+  }
+}
+
 size_t fwd_lds_bf16(const dfk_wattn_args& a, const Geo& g) {
   return 16 + 4 * (size_t)g.Np + 4 * (size_t)((g.L + 3) & ~3) + 4 * (size_t)g.Np * a.hd;
 }
@@ -1626,6 +1992,17 @@ size_t fwd_lds(const dfk_wattn_args& a, const Geo& g) {
 
 }  // namespace
 
+// dfk_wattn_fwd_policy (DFK_WATTN_V / DFK_WATTN_BALMIN set the start values for A/B runs)
+// defaults: v6; the balanced schedule from 512 units for v5, off for v6 (measured slower there: r5h, stage 1
+// 189.9 vs 178.5 us — the split phase's extra Q loads, barriers and spills cost more than the idle wave)
+static int g_fwd_version = getenv("DFK_WATTN_V") ? atoi(getenv("DFK_WATTN_V")) : 6;
+static long g_fwd_bal_min = getenv("DFK_WATTN_BALMIN") ? atol(getenv("DFK_WATTN_BALMIN")) : -1;   // -1: default
+
+// the forward reads its bias tiles in the 16x16x32 layout (wattn_fwd6_kernel) — the same predicate as dfk_wattn_fwd
+static bool fwd16_layout(const dfk_wattn_args& a, const Geo& g) {
+  return g_fwd_version == 6 && a.hd == 32 && !a.drop.mode && g.Np / 32 >= 2;
+}
+
 extern "C" int dfk_wattn_table(const dfk_wattn_args* ap, hipStream_t s) {
   if (!ap || !args_ok(*ap) || !ap->tab || ap->dtype != DFK_BF16 || ap->mask || !(ap->scale > 0.f)) return DFK_EINVAL;
   const dfk_wattn_args& a = *ap;
@@ -1634,18 +2011,15 @@ extern "C" int dfk_wattn_table(const dfk_wattn_args* ap, hipStream_t s) {
   bf16raw* t3 = tab3_fwd(a, g);
   hipLaunchKernelGGL(wattn_tab3_kernel, dim3((unsigned)std::min<long>(dfk_cdiv(2 * tg.per_ch / 8, 256), 64),
                                              tg.ncls * a.heads),
-                     dim3(256), 4 * (size_t)(g.Np + g.L), s, a, g, t3, t3 + tab_elems(a, g));
+                     dim3(256), 4 * (size_t)(g.Np + g.L), s, a, g, t3, t3 + tab_elems(a, g), fwd16_layout(a, g) ? 1 : 0);
   DFK_CHECK_LAUNCH();
   return 0;
 }
 
-// dfk_wattn_fwd_policy (DFK_WATTN_V / DFK_WATTN_BALMIN set the start values for A/B runs)
-static int g_fwd_version = getenv("DFK_WATTN_V") ? atoi(getenv("DFK_WATTN_V")) : 5;
-static long g_fwd_bal_min = getenv("DFK_WATTN_BALMIN") ? atol(getenv("DFK_WATTN_BALMIN")) : 512;
 
 extern "C" int dfk_wattn_fwd_policy(int32_t version, int64_t bal_min_units) {
   if (version >= 0) g_fwd_version = version;
-  if (bal_min_units >= 0) g_fwd_bal_min = (long)bal_min_units;
+  if (bal_min_units >= 0 || bal_min_units == -2) g_fwd_bal_min = bal_min_units >= 0 ? (long)bal_min_units : -1;
   return 0;
 }
 
@@ -1671,9 +2045,11 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     int qsplit = (int)std::max<long>(1, std::min<long>(dfk_cdiv(ngrp, nw), dfk_cdiv(1024, units)));
     // v5 (no running max; A/B: DFK_WATTN_V=4 keeps v4) and its balanced schedule (one workgroup per unit, the
     // remaining pairs and the tail split by keys over the 4 waves) from DFK_WATTN_BALMIN units (default 512)
-    const bool v5 = tab && a.hd == 32 && !a.drop.mode && qgrp == 2 && g_fwd_version >= 5;
+    const bool v6 = tab && a.hd == 32 && !a.drop.mode && qgrp == 2 && g_fwd_version == 6;
+    const bool v5 = tab && a.hd == 32 && !a.drop.mode && qgrp == 2 && g_fwd_version == 5;
     const int pairs = nqb / 2;
-    const bool bal = v5 && nw == 4 && pairs % 4 != 3 && units >= g_fwd_bal_min;
+    const long bal_min = g_fwd_bal_min >= 0 ? g_fwd_bal_min : (v5 ? 512 : LONG_MAX);
+    const bool bal = (v5 || v6) && nw == 4 && pairs % 4 != 3 && units >= bal_min;
     size_t lds_k = lds;
     if (bal) {
       qsplit = 1;
@@ -1694,6 +2070,8 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     if (a.hd == 32) {
       if (tab) {
         if (a.drop.mode) LAUNCH_K((wattn_fwd4_kernel<32, true, 1>));
+        else if (v6 && bal) LAUNCH_K((wattn_fwd6_kernel<true>));
+        else if (v6) LAUNCH_K((wattn_fwd6_kernel<false>));
         else if (bal) LAUNCH_K((wattn_fwd5_kernel<true>));
         else if (v5) LAUNCH_K((wattn_fwd5_kernel<false>));
         else if (qgrp == 2) LAUNCH_K((wattn_fwd4_kernel<32, false, 2>));
@@ -2365,8 +2743,8 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
 // sweeps every query block STAGGERED (wave w at step i takes block (i + w) mod nqb), so at each step the waves
 // add their partial dQ = dS K into distinct blocks of the fp32 LDS accumulator, behind one barrier per step (a
 // fixed add order: deterministic).  Per step (32 queries x 32 keys, queries on the MFMA row, keys on the lane):
-//   S' = Q' K^T + bias' - L'   (Q' = Q scale log2e, staged so in LDS; -L' = -lse log2e enters as the C input,
-//                               read from LDS; bias' by the identity product of the forward, bwd tile layout)
+//   S' = Q' K^T + bias' - L'   (Q' = Q scale log2e, staged so in LDS; bias' - L' enters as the C input: -lse log2e
+//                               read from LDS plus the bwd-layout bias tile unpacked on the VALU)
 //   dP' = dO V^T - delta        (-delta as the C input; delta = rowsum(dO O))
 //   P = 2^S', dS = P dP'        (dropout: dS = P (dP Z/keep - delta), P Z/keep into dV)
 //   dV^T += dO^T P, dK^T += Q'^T dS  (the score accumulators are the B operands: no lane movement)
@@ -2454,8 +2832,6 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   }
   __syncthreads();
 
-  bf16x8 id0, id1, sel;
-  bias_ident(lane, id0, id1, sel);
   bf16raw* Sw = Sd + wave * 32 * kSdRow;
   const DropCtx dc = drop_ctx(a.drop);
   bf16raw* dsu = dsg ? dsg + unit * Np * Np : nullptr;   // this window-head's dS^T [k][q]
@@ -2524,6 +2900,19 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
           dp[4 * v + t] = DROP ? 0.f : d4[t];
         }
       }
+      if constexpr (TAB) {   // bias' (C-input layout: element 8c + j of the lane's key) added to -L'
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const uint4 w4 = __builtin_bit_cast(uint4, bt[c]);
+          const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            s[8 * c + 2 * i] += __uint_as_float(w[i] << 16);
+            s[8 * c + 2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
+          }
+        }
+        load_bias(qb + 1 == nqb ? 0 : qb + 1);
+      }
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
         const int off = qr0 * HD + qoff[kk];
@@ -2532,11 +2921,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
         s = mfma32(qa, kB[kk], s);
         dp = mfma32(da, vB[kk], dp);
       }
-      if constexpr (TAB) {
-        s = mfma32(bt[0], id0, s);
-        s = mfma32(bt[1], id1, s);
-        load_bias(qb + 1 == nqb ? 0 : qb + 1);
-      }
+
       // P = 2^S', dS = P dP'; B-operand fragments of k-steps c (registers 8c .. 8c+7)
       bf16x8 pa[2], sa[2];
 #pragma unroll

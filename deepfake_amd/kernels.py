@@ -315,8 +315,9 @@ def wattn_fwd(q, k, v, ld_qkv, dims, window, full_window, shift, heads, hd, scal
 
 
 def wattn_fwd_policy(version=-1, bal_min_units=-1):
-    """Process-wide kernel choice of the hd-32 bf16 table forward (tests / A/B runs): version 5 (no running max,
-    default) or 4; bal_min_units = smallest launch on the balanced key-split schedule. -1 leaves a setting."""
+    """Process-wide kernel choice of the hd-32 bf16 table forward (tests / A/B runs): version 6 (no running max,
+    16x16x32 tiles, default), 5 (32x32x16) or 4 (max-subtracted); bal_min_units = smallest launch on the balanced
+    key-split schedule. -1 leaves a setting, -2 restores the default.  The bias table must be built under the same policy as the forward."""
     L.check(L.lib().dfk_wattn_fwd_policy(int(version), int(bal_min_units)), "wattn_fwd_policy")
 
 

@@ -203,9 +203,11 @@ typedef struct {
 } dfk_wattn_args;
 int dfk_wattn_fwd(const dfk_wattn_args* a, hipStream_t stream);
 /* kernel-selection policy of dfk_wattn_fwd's hd-32 table path (process-wide; tests and A/B runs only — the
- * defaults are the product's choice): version 5 = no-running-max forward (default), 4 = the max-subtracted
- * forward; bal_min_units = smallest launch (units = clips x windows x heads) that runs the key-split balanced
- * schedule (default 512).  A negative argument leaves that setting unchanged.  Returns 0. */
+ * defaults are the product's choice): version 6 = no-running-max forward on 16x16x32 tiles (default), 5 = the
+ * same on 32x32x16 tiles, 4 = the max-subtracted forward; bal_min_units = smallest launch (units = clips x windows
+ * x heads) that runs the key-split balanced schedule (default: 512 for version 5, never for version 6).  -1
+ * leaves a setting unchanged, bal_min_units -2 restores its default.  Returns 0.  dfk_wattn_table builds its forward bias tiles in
+ * the layout of the version in force, so a table must come from the same policy as the forward that reads it. */
 int dfk_wattn_fwd_policy(int32_t version, int64_t bal_min_units);
 int64_t dfk_wattn_table_workspace(const dfk_wattn_args* a);
 /* builds a->tab (fwd and bwd layouts) from a->rpb, the shift and the window geometry

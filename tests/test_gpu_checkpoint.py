@@ -101,31 +101,28 @@ def test_c5_long_clip_checkpointed():
         del m, p, loss
         torch.cuda.empty_cache()
     (la, ga, pa), (lb, gb, pb), (_, gb2, _) = out["ck"], out["plain"], out["plain2"]
-    # the forward is reproducible (the wav2vec2 conv0 GroupNorm statistics are summed in a fixed order since r4;
-    # they were fp32 atomics, which moved the loss by up to 1.8e-5 between identical forwards): 1e-5 stays as slack
-    assert torch.isfinite(torch.tensor(la)) and abs(la - lb) <= 1e-5 * max(1.0, abs(lb)), (la, lb)
+    # the forward is bitwise reproducible (profiles/r5/r5a_determinism_c2_bf16.txt: identical loss and logits over
+    # two runs; the gradients of identical runs differ only by fp32 atomic order in weight-gradient sums, <= 3.5e-6
+    # relative per tensor, 5.3e-8 relative L2): the checkpointed recompute runs the same kernels on the same
+    # inputs, so the loss must agree to fp32 rounding and every gradient to atomic-order noise
+    assert torch.isfinite(torch.tensor(la)) and abs(la - lb) <= 1e-6 * max(1.0, abs(lb)), (la, lb)
     assert ga.keys() == gb.keys() and len(ga) > 300
 
     def rel(x, y):
         return ((x - y).abs().max() / y.abs().max().clamp_min(1e-12)).item()
-    # bar: 2e-2 (bf16), or 3x the run-to-run spread of the un-checkpointed model itself for tensors whose
-    # gradient is a near-cancelling sum (order-dependent fp32 atomics upstream, then bf16 rounding)
-    # tensors whose gradient is analytically zero (attention key biases: softmax is invariant to a per-query
-    # shift, so d/db_k = sum_q q (sum_k dS) = 0) hold bf16 rounding noise only: relative errors of noise are
-    # meaningless there, so they are held to an absolute bound against the model's largest gradient instead
-    # the noise figure is itself one draw (one pair of plain runs), so a single tensor may land a few times above
-    # it by chance: every tensor is held to 6x (and 6e-2), and at most 1 % of them may exceed 3x (and 2e-2) —
-    # a checkpointing bug (a wrong recompute) moves many tensors far outside, not one near-cancelling sum
+    # bar per tensor: 1e-4 relative (about 30x the largest atomic-order difference measured between identical
+    # runs), or 6x this run pair's own spread; tensors whose gradient is analytically zero (attention key biases:
+    # softmax is invariant to a per-query shift) hold rounding noise only and are held to an absolute bound against
+    # the model's largest gradient instead.  A checkpointing bug (a wrong recompute) moves tensors by orders more.
     top = max(float(g.abs().max()) for g in gb.values())
-    over = []
+    worst = (0.0, None)
     for n in gb:
         e, noise = rel(ga[n], gb[n]), rel(gb2[n], gb[n])
         if noise > 0.5 or float(gb[n].abs().max()) < 1e-4 * top:   # noise-dominated: analytically zero
             assert float(ga[n].abs().max()) < 1e-3 * top, (n, float(ga[n].abs().max()), top)
             continue
-        assert e <= max(6e-2, 6 * noise), (n, e, noise)
-        if e > max(2e-2, 3 * noise):
-            over.append((n, e, noise))
-    assert len(over) <= len(gb) // 100, over
+        assert e <= max(1e-4, 6 * noise), (n, e, noise)
+        worst = max(worst, (e, n))
+    print(f"C5 checkpointed vs plain: worst gradient tensor {worst}")
     print(f"C5 B=2 peak activation memory: checkpointed {pa / 2**30:.2f} GiB, plain {pb / 2**30:.2f} GiB")
     assert pa < pb

@@ -143,10 +143,10 @@ V5_CASES = [
     ((1, 3, 14, 14), (3, 7, 7), (1, 3, 3), 2),    # N 147: 5 blocks, pairs 2 (R 2) + tail
     ((1, 4, 14, 14), (4, 7, 7), (2, 3, 3), 2),    # N 196: 7 blocks, pairs 3 (R 3: simple schedule)
 ]
-V5_POLICIES = [(5, 0), (5, 1 << 40), (4, -1)]   # balanced, simple, v4
+V5_POLICIES = [(5, 0), (5, 1 << 40), (4, -1), (6, 0), (6, 1 << 40)]   # v5 balanced / simple, v4, v6 balanced / simple
 
 
-@pytest.mark.parametrize("policy", V5_POLICIES, ids=["v5bal", "v5", "v4"])
+@pytest.mark.parametrize("policy", V5_POLICIES, ids=["v5bal", "v5", "v4", "v6bal", "v6"])
 @pytest.mark.parametrize("extreme", ["normal", "huge", "tiny"])
 @pytest.mark.parametrize("case", V5_CASES, ids=[str(i) for i in range(len(V5_CASES))])
 def test_wattn_fwd_v5(case, extreme, policy):
@@ -176,7 +176,7 @@ def test_wattn_fwd_v5(case, extreme, policy):
         out4, lse4 = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, window, window, shift, heads, hd,
                                  scale, rpb=rpb, pads=pads)
     finally:
-        K.wattn_fwd_policy(5, 512)
+        K.wattn_fwd_policy(6, -2)   # the defaults (dfk_wattn_fwd_policy)
     torch.cuda.synchronize()
     if extreme == "normal":
         ref = ref_attention(qkv, pads, dims, window, window, shift, heads, hd, scale, rpb)

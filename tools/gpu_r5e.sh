@@ -3,5 +3,5 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 rm -f gpurun_out/exp/log.txt
-bash tools/exp_run.sh "python -u tools/wattn_bench.py 20" base NOBIAS NOKV NOBIASKV NOQK NOEXP NOPV > /dev/null 2>&1 || { tail -20 gpurun_out/exp/log.txt; exit 1; }
+bash tools/exp_run.sh "python -u tools/wattn_bench.py 20" base ABL NOBIAS NOQK NOEXP NOPV NOBIASEXP > /dev/null 2>&1 || { tail -20 gpurun_out/exp/log.txt; exit 1; }
 grep "==\|vst1\|vst3" gpurun_out/exp/log.txt
