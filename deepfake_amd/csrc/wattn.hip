@@ -1999,9 +1999,15 @@ static int g_fwd_version = getenv("DFK_WATTN_V") ? atoi(getenv("DFK_WATTN_V")) :
 static long g_fwd_bal_min = getenv("DFK_WATTN_BALMIN") ? atol(getenv("DFK_WATTN_BALMIN")) : -1;   // -1: default
 
 // the forward reads its bias tiles in the 16x16x32 layout (wattn_fwd6_kernel) — the same predicate as dfk_wattn_fwd
-static bool fwd16_layout(const dfk_wattn_args& a, const Geo& g) {
-  return g_fwd_version == 6 && a.hd == 32 && !a.drop.mode && g.Np / 32 >= 2;
+// v6 runs windows of at least 4 query blocks (Np >= 128: every Video Swin stage); the 49-token SwinV2 windows keep
+// v4 — v6 gains nothing there (mel1: 14.5-15.7 vs 15.5 us) and v4's rounding keeps the SwinV2 logit_scale gradients
+// where the goldens hold them (r5j: C1 mel layers.1.blocks.1 logit_scale norm 5.7 % with v4, 8.6 % with v6, against
+// 1.1 % in the reference's own bf16 run — the same attention error, rms 2.8e-3 either way, tools/wattn_err.py, in a
+// gradient that cancels to a few % of its terms)
+static bool use_v6(const dfk_wattn_args& a, const Geo& g) {
+  return g_fwd_version == 6 && a.hd == 32 && !a.drop.mode && g.Np / 32 >= 4;
 }
+static bool fwd16_layout(const dfk_wattn_args& a, const Geo& g) { return use_v6(a, g); }
 
 extern "C" int dfk_wattn_table(const dfk_wattn_args* ap, hipStream_t s) {
   if (!ap || !args_ok(*ap) || !ap->tab || ap->dtype != DFK_BF16 || ap->mask || !(ap->scale > 0.f)) return DFK_EINVAL;
@@ -2045,8 +2051,8 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     int qsplit = (int)std::max<long>(1, std::min<long>(dfk_cdiv(ngrp, nw), dfk_cdiv(1024, units)));
     // v5 (no running max; A/B: DFK_WATTN_V=4 keeps v4) and its balanced schedule (one workgroup per unit, the
     // remaining pairs and the tail split by keys over the 4 waves) from DFK_WATTN_BALMIN units (default 512)
-    const bool v6 = tab && a.hd == 32 && !a.drop.mode && qgrp == 2 && g_fwd_version == 6;
-    const bool v5 = tab && a.hd == 32 && !a.drop.mode && qgrp == 2 && g_fwd_version == 5;
+    const bool v6 = tab && qgrp == 2 && use_v6(a, g);
+    const bool v5 = tab && a.hd == 32 && !a.drop.mode && qgrp == 2 && g_fwd_version == 5;   // v4 otherwise
     const int pairs = nqb / 2;
     const long bal_min = g_fwd_bal_min >= 0 ? g_fwd_bal_min : (v5 ? 512 : LONG_MAX);
     const bool bal = (v5 || v6) && nw == 4 && pairs % 4 != 3 && units >= bal_min;
