@@ -375,6 +375,9 @@ class WindowAttnFn(torch.autograd.Function):
         out, lse, tab = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], qkv.stride(0), dims, window, full_window, shift,
                                     heads, hd, scale, rpb=rpb_f, pads=pads, mask=mask, return_table=True, drop=drop)
         ctx.tab = tab
+        # a batched CPB table (Fn.cpb_tables) hands its slice of the shared gradient buffer to its first consumer
+        # only: a second consumer of the same table gets a fresh gradient, which autograd adds out of place
+        ctx.gview = rpb.__dict__.pop("_dfk_gview", None) if rpb is not None else None
         grad_use(ctx, 1, rpb)
         grad_use(ctx, 2, qkv_bias)
         ctx.save_for_backward(qkv, out, lse, rpb_f, mask, rpb, qkv_bias)
@@ -390,7 +393,11 @@ class WindowAttnFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         drpb = None
         if ctx.has_rpb:
-            drpb = grad_sink(rpb) if rpb.dtype == torch.float32 and rpb.is_contiguous() else torch.zeros_like(rpb_f)
+            if ctx.gview is not None:      # a batched CPB table: its zeroed slice of the shared gradient buffer
+                drpb = ctx.gview
+            else:
+                drpb = grad_sink(rpb) if rpb.dtype == torch.float32 and rpb.is_contiguous() else torch.zeros_like(rpb_f)
+            ctx.gview = None
         dbias = grad_sink(qkv_bias) if ctx.has_bias else None
         dpads = [dbias[i * C:(i + 1) * C] for i in range(3)] if ctx.has_bias else None
         K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, qkv.stride(0), dims, window, full_window, shift, heads,
@@ -685,15 +692,28 @@ class CPBManyFn(torch.autograd.Function):
             grad_use(ctx, 1 + n + i, p)
         ctx.n, ctx.dims, ctx.maxL, ctx.fwd_rows = n, dims, maxL, fwd_rows
         ctx.save_for_backward(out, *cs, *ws, *params)   # cs / ws: the descriptor's pointers stay valid
-        return tuple(out[o:o + L * h].view(L, h) for o, L, h in dims)
+        # one zeroed fp32 buffer for all tables' gradients: each block's attention backward accumulates its dRPB
+        # into its slice (WindowAttnFn reads t._dfk_gview) — one fill per step instead of one per block, and the
+        # backward below finds the gradients already contiguous (no cat)
+        ctx.gbuf = torch.zeros_like(out)
+        tabs = tuple(out[o:o + L * h].view(L, h) for o, L, h in dims)
+        for t, (o, L, h) in zip(tabs, dims):
+            t._dfk_gview = ctx.gbuf[o:o + L * h].view(L, h)
+        return tabs
 
     @staticmethod
     def backward(ctx, *douts):
         saved = ctx.saved_tensors
         n = ctx.n
         out, params = saved[0], saved[1 + n + 3 * n:]
-        dflat = torch.cat([(d if d is not None else torch.zeros(L, h, device=out.device)).float().reshape(-1)
-                           for d, (o, L, h) in zip(douts, ctx.dims)])
+        base = ctx.gbuf.data_ptr() if ctx.gbuf is not None else -1
+        if base >= 0 and all(d is not None and d.dtype == torch.float32 and d.data_ptr() == base + 4 * o
+               for d, (o, L, h) in zip(douts, ctx.dims)):
+            dflat = ctx.gbuf   # every block accumulated into its slice of the shared buffer
+        else:
+            dflat = torch.cat([(d if d is not None else torch.zeros(L, h, device=out.device)).float().reshape(-1)
+                               for d, (o, L, h) in zip(douts, ctx.dims)])
+        ctx.gbuf = None
         sinks = [grad_sink(p) for p in params]
         rows = [r[:4] + [t.data_ptr() for t in sinks[3 * i:3 * i + 3]] + r[7:] for i, r in enumerate(ctx.fwd_rows)]
         K.L.check(K.L.lib().dfk_cpb_bias_bwd_many(K.L.ptr(_cpb_desc(rows)), n, ctx.maxL, K.L.ptr(out),
