@@ -175,6 +175,8 @@ def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None, residual=No
 
 
 _DW_MIN_K = int(os.environ.get("DFK_DW_MINK", "512"))   # tokens per split of a weight-gradient GEMM (tuning)
+_DW_UNSPLIT64 = int(os.environ.get("DFK_DW_UNSPLIT64", "384"))   # 64x64 tiles from which dW runs unsplit (r5o: the
+# 256-tile SwinV2 stage-3 fc1 / fc2 dW 22 -> 19, 21 -> 19 us on split 128x128 tiles; w2v (432-576 tiles) flat)
 _DW_XCD = int(os.environ.get("DFK_DW_XCD", "1"))   # split counts rounded to multiples of 8 (XCD grouping; A/B knob)
 
 
@@ -189,7 +191,7 @@ def linear_dw(dy, x, dw, db=None):
     epilogue; skinny ones split the M reduction and add fp32 partials atomically."""
     M, N = dy.shape
     K = x.shape[1]
-    if math.ceil(N / 64) * math.ceil(K / 64) >= 256:
+    if math.ceil(N / 64) * math.ceil(K / 64) >= _DW_UNSPLIT64:
         gemm(dy, dy.stride(0), True, x, x.stride(0), True, N, K, M, dw, dw.stride(0), dtype=L.dt(dy), c_f32=True,
              beta=1.0, rowsum=db)
         return dw
