@@ -144,9 +144,9 @@ def test_inlaunch_combine(dt, M, N, Kd, monkeypatch):
     monkeypatch.setenv("DFK_INLAUNCH_COMBINE", "1")
     got = run()
     for i, (a, b) in enumerate(zip(got, base)):
-        if i < 4:
+        if i < 4 and i != 2:
             assert torch.equal(a, b), i
-        else:   # group sums added atomically: the order of the per-group atomics differs
+        else:   # group sums (and the dW of a split 128x128 grid: K.linear_dw) added atomically: order differs
             assert rel(a, b) < 1e-5, i
 
 
