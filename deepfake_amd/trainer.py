@@ -138,10 +138,12 @@ class TrainStep:
         if not bucketer.bn_buffers:
             bucketer.track_batchnorm(model)
 
-    def _fwd_bwd(self, feature, label, scale=1.0):
+    def _fwd_bwd(self, feature, label, scale=1.0, before_backward=None):
         rng.advance(self.store.flat.device)   # fresh dropout / DropPath / LayerDrop / SpecAugment draws
         prob = self.model(feature)
         loss = self.lossF(prob.float().reshape(-1), label.float().reshape(-1))
+        if before_backward is not None:
+            before_backward()
         (loss * scale if scale != 1.0 else loss).backward()
         if getattr(self.model, "parallel_branches", False):
             self.model.join_branches()
@@ -295,13 +297,17 @@ class TrainStep:
 
     def _step_body(self, static_in, static_label, accum):
         """The optimizer step's graph body: (zeroing,) BN broadcast, fwd + bwd, all-reduces, SGD."""
+        late = accum == 1 and os.environ.get("DFK_ZERO_LATE", "0") == "1"   # A/B: zero the gradients after the forward
+
         def body(overlap, bn):
             if accum == 1:
-                self.store.grad.zero_()
+                if not late:
+                    self.store.grad.zero_()
                 self.store.zero_gates()
                 if bn:
                     self.bucketer.broadcast_bn()
-            l2, p2 = self._fwd_bwd(tuple(static_in), static_label, 1.0 / accum)
+            l2, p2 = self._fwd_bwd(tuple(static_in), static_label, 1.0 / accum,
+                                   before_backward=self.store.grad.zero_ if late else None)
             fold = self._fold()
             if overlap:
                 fa = self.bucketer.finish(fold=fold)   # flush unused buckets, join the comm stream
