@@ -297,17 +297,27 @@ class TrainStep:
 
     def _step_body(self, static_in, static_label, accum):
         """The optimizer step's graph body: (zeroing,) BN broadcast, fwd + bwd, all-reduces, SGD."""
-        late = accum == 1 and os.environ.get("DFK_ZERO_LATE", "0") == "1"   # A/B: zero the gradients after the forward
+        # where the step graph zeroes the gradients (A/B): 0 at the start, 1 after the forward, 2 on a side stream
+        # beside the forward (joined before the backward)
+        zmode = int(os.environ.get("DFK_ZERO_MODE", "0")) if accum == 1 else 0
 
         def body(overlap, bn):
+            join = None
             if accum == 1:
-                if not late:
+                if zmode == 0:
                     self.store.grad.zero_()
+                elif zmode == 2:
+                    zs = self._side_stream()
+                    zs.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(zs):
+                        self.store.grad.zero_()
+                    join = lambda: torch.cuda.current_stream().wait_stream(zs)   # noqa: E731
+                else:
+                    join = self.store.grad.zero_
                 self.store.zero_gates()
                 if bn:
                     self.bucketer.broadcast_bn()
-            l2, p2 = self._fwd_bwd(tuple(static_in), static_label, 1.0 / accum,
-                                   before_backward=self.store.grad.zero_ if late else None)
+            l2, p2 = self._fwd_bwd(tuple(static_in), static_label, 1.0 / accum, before_backward=join)
             fold = self._fold()
             if overlap:
                 fa = self.bucketer.finish(fold=fold)   # flush unused buckets, join the comm stream
@@ -319,6 +329,11 @@ class TrainStep:
                 self.store.zero_gates()
             return l2.detach(), p2.detach()
         return body
+
+    def _side_stream(self):
+        if getattr(self, "_zstream", None) is None:
+            self._zstream = torch.cuda.Stream()
+        return self._zstream
 
     def _fallback(self, err):
         self.graph_mode = False
