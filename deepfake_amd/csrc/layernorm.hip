@@ -44,6 +44,37 @@ __device__ __forceinline__ void store8(T* p, const float (&v)[8]) {
   }
 }
 
+// raw 8-element vectors: the loads of a row group are issued as early as possible and converted when used
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16raw> { uint4 u; };
+template <> struct Raw8<float> { float4 a, b; };
+
+template <typename T>
+__device__ __forceinline__ Raw8<T> ld_raw(const T* base, long off, bool ok) {
+  const T* p = base + (ok ? off : 0);
+  Raw8<T> r;
+  if constexpr (sizeof(T) == 2) {
+    r.u = *reinterpret_cast<const uint4*>(p);
+  } else {
+    r.a = *reinterpret_cast<const float4*>(p);
+    r.b = *reinterpret_cast<const float4*>(p + 4);
+  }
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ void unraw(const Raw8<T>& r, bool ok, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16raw* e = reinterpret_cast<const bf16raw*>(&r.u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = ok ? bf2f(e[i]) : 0.f;
+  } else {
+    const float t[8] = {r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = ok ? t[i] : 0.f;
+  }
+}
+
 template <int L>
 __device__ __forceinline__ float group_sum(float v) {
 #pragma unroll
@@ -65,6 +96,12 @@ __global__ __launch_bounds__(256) void ln_fwd(const T* __restrict__ x, const T* 
   const long roff = rok ? row * C : 0;
   float v[V][8];
   float s = 0.f;
+  // the residual rows are loaded with x (one HBM round trip per row group, not two)
+  Raw8<T> rr[V];
+  if (res) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) rr[i] = ld_raw<T>(res, roff + (li + i * L) * 8, rok && li + i * L < nv);
+  }
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int vi = li + i * L;
@@ -101,7 +138,7 @@ __global__ __launch_bounds__(256) void ln_fwd(const T* __restrict__ x, const T* 
     }
     if (res) {
       float rv[8];
-      load8m<T>(res, roff + vi * 8, rok && ok, rv);
+      unraw<T>(rr[i], rok && ok, rv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] += rv[e];
     }
@@ -114,14 +151,13 @@ __global__ __launch_bounds__(256) void ln_fwd(const T* __restrict__ x, const T* 
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g*xhat)),  g = dy*w ; dw += dy*xhat ; db += dy
-template <typename T, int L, int V>
+template <typename T, int L, int V, bool TWO>
 __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T* __restrict__ x,
                                               const T* __restrict__ w, const float* __restrict__ mean,
                                               const float* __restrict__ rstd, T* __restrict__ dx, float* dw,
                                               float* db, long rows, int C, int accumulate, float* __restrict__ part,
                                               const dfk_drop drop, uint32_t* cnt, int gs, const T* __restrict__ addend) {
   constexpr int RPW = 64 / L;
-  constexpr bool KEEP = V <= 4;   // x, dy stay in registers between the two sweeps
   extern __shared__ float red[];  // [2][C] block partials of dw, db
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane % L;
@@ -138,39 +174,58 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
   __syncthreads();
   const DropCtx dc = drop_ctx(drop);   // the forward's mask on dy (gradient of drop(LN(x)))
   const long step = (long)gridDim.x * 4 * RPW;
-  for (long r0 = ((long)blockIdx.x * 4 + wave) * RPW; r0 < rows; r0 += step) {
+  const bool add = addend || accumulate;
+  const T* aptr = addend ? addend : dx;
+  // A row group's operands — x, dy, the addend (or dx when accumulating), mean, rstd — as raw registers, all
+  // loaded at once.  Narrow rows (bf16, V <= 2: every Swin stage-1/2 and SwinV2 LayerNorm) keep two groups in
+  // flight: the wave's next-but-one group is loaded right after the current one is consumed (two register sets,
+  // the loop unrolled by two, no copy of a register with a load in flight).
+  struct Grp {
+    Raw8<T> x[V], d[V], a[V];
+    float mu, rs;
+  };
+  auto fetch = [&](Grp& gp, long r0) __attribute__((always_inline)) {
     const long row = r0 + lane / L;
     const bool rok = row < rows;
     const long roff = rok ? row * C : 0;
-    const float mu = mean[rok ? row : 0], rs = rstd[rok ? row : 0];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int vi = li + i * L;
+      const bool ok = rok && vi < nv;
+      gp.x[i] = ld_raw<T>(x, roff + vi * 8, ok);
+      gp.d[i] = ld_raw<T>(dy, roff + vi * 8, ok);
+      if (add) gp.a[i] = ld_raw<T>(aptr, roff + vi * 8, ok);
+    }
+    gp.mu = mean[rok ? row : 0];
+    gp.rs = rstd[rok ? row : 0];
+  };
+  auto process = [&](const Grp& gp, long r0) __attribute__((always_inline)) {
+    const long row = r0 + lane / L;
+    const bool rok = row < rows;
+    const float mu = gp.mu, rs = gp.rs;
     const float gmul = dc.mode == 2 ? drop_mul(dc, row, 0) : 1.f;
-    auto dmask = [&](float (&dv)[8], int vi) {
-      if (dc.mode == 2) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dv[e] *= gmul;
-      } else if (dc.mode == 1) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dv[e] *= drop_mul(dc, row, vi * 8 + e);
-      }
-    };
-    float xs[KEEP ? V : 1][8], ds[KEEP ? V : 1][8];
+    float xs[V][8], ds[V][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       const int vi = li + i * L;
       const bool ok = rok && vi < nv;
-      float xv[8], dv[8];
-      load8m<T>(x, roff + vi * 8, ok, xv);
-      load8m<T>(dy, roff + vi * 8, ok, dv);
-      dmask(dv, vi);
+      unraw<T>(gp.x[i], ok, xs[i]);
+      unraw<T>(gp.d[i], ok, ds[i]);
+      if (dc.mode == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ds[i][e] *= gmul;
+      } else if (dc.mode == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ds[i][e] *= drop_mul(dc, row, vi * 8 + e);
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float xh = (xv[e] - mu) * rs, g = dv[e] * wv[i][e];
+        const float xh = (xs[i][e] - mu) * rs, g = ds[i][e] * wv[i][e];
         s1 += g;
         s2 += g * xh;
-        pw[i][e] += ok ? dv[e] * xh : 0.f;
-        pb[i][e] += dv[e];
-        if constexpr (KEEP) { xs[i][e] = xv[e]; ds[i][e] = dv[e]; }
+        pw[i][e] += ok ? ds[i][e] * xh : 0.f;
+        pb[i][e] += ds[i][e];
       }
     }
     const float m1 = group_sum<L>(s1) / C, m2 = group_sum<L>(s2) / C;
@@ -178,25 +233,36 @@ __global__ __launch_bounds__(256) void ln_bwd(const T* __restrict__ dy, const T*
     for (int i = 0; i < V; ++i) {
       const int vi = li + i * L;
       const bool ok = rok && vi < nv;
-      float xv[8], dv[8], o[8];
-      if constexpr (KEEP) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { xv[e] = xs[i][e]; dv[e] = ds[i][e]; }
-      } else {
-        load8m<T>(x, roff + vi * 8, ok, xv);
-        load8m<T>(dy, roff + vi * 8, ok, dv);
-        dmask(dv, vi);
-      }
-      const bool add = addend || accumulate;
-      if (addend) load8m<T>(addend, roff + vi * 8, ok, o);
-      else if (accumulate) load8m<T>(dx, roff + vi * 8, ok, o);
+      float o[8];
+      if (add) unraw<T>(gp.a[i], ok, o);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float xh = (xv[e] - mu) * rs;
-        const float d = rs * (dv[e] * wv[i][e] - m1 - xh * m2);
+        const float xh = (xs[i][e] - mu) * rs;
+        const float d = rs * (ds[i][e] * wv[i][e] - m1 - xh * m2);
         o[e] = add ? o[e] + d : d;
       }
       if (ok) store8<T>(dx + row * C + vi * 8, o);
+    }
+  };
+  long r0 = ((long)blockIdx.x * 4 + wave) * RPW;
+  if constexpr (TWO) {   // two groups in flight (a separate instantiation: its registers cost the one-group form occupancy)
+    Grp ga, gb;
+    fetch(ga, r0);
+    fetch(gb, r0 + step);
+    while (r0 < rows) {
+      process(ga, r0);
+      fetch(ga, r0 + 2 * step);   // past the end: clamped to row 0, masked
+      r0 += step;
+      if (r0 >= rows) break;
+      process(gb, r0);
+      fetch(gb, r0 + 2 * step);
+      r0 += step;
+    }
+  } else {
+    for (; r0 < rows; r0 += step) {
+      Grp gp;
+      fetch(gp, r0);
+      process(gp, r0);
     }
   }
   // dw / db partials: sum the RPW row groups of the wave, then the waves of the block through LDS
@@ -322,9 +388,16 @@ void bwd_launch(const void* dy, const void* x, const void* w, const float* mean,
   int gs = 64;
   while (gs > 8 && (long)gs * 8 * C > 49152) gs >>= 1;
   uint32_t* cnt = part ? dfk_ticket_slice(dfk_cdiv(blocks, gs), s) : nullptr;
-  hipLaunchKernelGGL((ln_bwd<T, L, V>), dim3(blocks), dim3(256), 2 * C * sizeof(float), s, (const T*)dy,
-                     (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part, drop, cnt, gs,
-                     (const T*)addend);
+  // two row groups in flight when the waves loop (bf16 rows of at most 2 x 64 x 8 channels)
+  const bool two = sizeof(T) == 2 && V <= 2 && rows > (long)blocks * 4 * (64 / L);
+  if (two)
+    hipLaunchKernelGGL((ln_bwd<T, L, V, (sizeof(T) == 2 && V <= 2)>), dim3(blocks), dim3(256), 2 * C * sizeof(float), s,
+                       (const T*)dy, (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part,
+                       drop, cnt, gs, (const T*)addend);
+  else
+    hipLaunchKernelGGL((ln_bwd<T, L, V, false>), dim3(blocks), dim3(256), 2 * C * sizeof(float), s, (const T*)dy,
+                       (const T*)x, (const T*)w, mean, rstd, (T*)dx, dw, db, rows, C, accumulate, part, drop, cnt, gs,
+                       (const T*)addend);
   if (part && !cnt)
     hipLaunchKernelGGL(slab_colsum, dim3(dfk_cdiv(2 * C, 64), dfk_cdiv(blocks, 256)), dim3(256), 0, s, part, blocks, C,
                        dw, db);

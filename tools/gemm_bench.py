@@ -67,13 +67,15 @@ def main():
         tg = t(lambda: K.linear(x, w, out=out, act=1, aux=aux))
         tx = t(lambda: K.linear_dx(dy, w, out=dx))
         tw = t(lambda: K.linear_dw(dy, x, dw))
+        dbias = torch.zeros(N, device="cuda")
+        twb = t(lambda: K.linear_dw(dy, x, dw, dbias))   # with the fused bias gradient (the training step's form)
         tot["fwd"] += tf
         tot["dx"] += tx
         tot["dw"] += tw
         bytes_f = (M * Kd + M * N + N * Kd) * x.element_size()
         print(f"{name:10s} M={M:7d} N={N:5d} K={Kd:5d}  fwd {fl / tf / 1e12:7.1f} TF ({bytes_f / tf / 1e9:6.0f} GB/s)"
               f"  dx {fl / tx / 1e12:7.1f} TF  dw {fl / tw / 1e12:7.1f} TF   [{tf * 1e6:.0f}/{tx * 1e6:.0f}/{tw * 1e6:.0f} us]"
-              f"  gelu+aux {tg * 1e6:.0f} us",
+              f"  gelu+aux {tg * 1e6:.0f} us  dw+db {twb * 1e6:.0f} us",
               flush=True)
         if a.torch:
             rf = t(lambda: torch.nn.functional.linear(x, w))

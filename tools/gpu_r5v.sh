@@ -11,3 +11,5 @@ for i in 1 2; do
 timeout -k 10 300 python3 -u bench.py --no-cpu-baseline > $OUT/b$i.json 2> $OUT/b$i.err || { tail -20 $OUT/b$i.err; exit 1; }
 echo "$(cut -c90-175 $OUT/b$i.json)"
 done
+timeout -k 10 200 python -u tools/gemm_bench.py --only w2v,mel3,vst1,vst2 > $OUT/gemm.txt 2>&1 || { tail -20 $OUT/gemm.txt; exit 1; }
+grep -v amdgpu.ids $OUT/gemm.txt
