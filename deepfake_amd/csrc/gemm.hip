@@ -673,10 +673,14 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_rs = RS && tn == 0 && wn == 0;
-  f32x4 accr[MI];
+  // fused row sums of A (bias gradients) in the first column of tiles, shared by the wave columns: wave column wn
+  // takes fragments mi = h NWN + wn (one wave column doing all of them held every k-tile's barrier for its extra
+  // MFMAs: stage-1 dW + db 120 -> 137 us)
+  constexpr int MH = (MI + NWN - 1) / NWN;
+  const bool do_rs = RS && tn == 0;
+  f32x4 accr[MH];
 #pragma unroll
-  for (int i = 0; i < MI; ++i) accr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MH; ++i) accr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
   for (int d = 0; d < S - 1; ++d)
@@ -717,23 +721,64 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm
 #pragma unroll
         for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
 #pragma unroll
-        for (int mi = 0; mi < MI; ++mi) accr[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], ones, accr[mi], 0, 0, 0);
+        for (int h = 0; h < MH; ++h) {
+          bf16x8 a = af[h * NWN < MI ? h * NWN : MI - 1];
+#pragma unroll
+          for (int c = 1; c < NWN; ++c)
+            if (wn == c && h * NWN + c < MI) a = af[h * NWN + c];
+          accr[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones, accr[h], 0, 0, 0);
+        }
       }
     }
   }
   if (RS && do_rs && (lane & 15) == 0) {
+    // atomic split-K (the workspace holds [splitk][M] partials): one plain store per (split, row), summed by
+    // rowsum_reduce_kernel — the splits' same-address atomics on the few cache lines of the bias gradient
+    // serialised (stage-1 dW + db 120 -> 137 us, proj 41 -> 66 us)
+    float* rsp = g.atomic && g.splitk > 1 && g.ws ? reinterpret_cast<float*>(g.ws) + (long)split * g.M : nullptr;
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi)
+    for (int h = 0; h < MH; ++h) {
+      const int mi = h * NWN + wn;
+      if (mi < MI)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = bm + wm * WT + mi * 16 + (lane >> 4) * 4 + r;
-        if (row < g.M) atomicAdd(g.rowsum + row, accr[mi][r]);
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int row = bm + wm * WT + mi * 16 + (lane >> 4) * 4 + r;
+          if (row < g.M) {
+            if (rsp) rsp[row] = accr[h][r];
+            else atomicAdd(g.rowsum + row, accr[h][r]);
+          }
+        }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   tile_epilogue<bf16raw, WT>(g, smem_f, acc, lane, wave, wm, wn, bm, bn, z, split,
                              (z * (int)gridDim.y + tmi) * (int)gridDim.x + tn, evec, sk);
+}
+
+// rowsum[row] += sum over splits of part[split][row] (the bias gradient of an atomic split-K dW, fixed order):
+// 64 rows per workgroup, 16 split phases (each thread sums every 16th split, 4 loads in flight), folded in LDS
+__global__ __launch_bounds__(1024) void rowsum_reduce_kernel(const float* __restrict__ part, int splitk, int M,
+                                                             float* __restrict__ rowsum) {
+  __shared__ float red[16][64];
+  const int c = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int row = blockIdx.x * 64 + c;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (row < M) {
+    int sp = ph;
+    for (; sp + 48 < splitk; sp += 64)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += part[(long)(sp + 16 * u) * M + row];
+    for (; sp < splitk; sp += 16) a[0] += part[(long)sp * M + row];
+  }
+  red[ph][c] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (ph == 0 && row < M) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c];
+    rowsum[row] += t;
+  }
 }
 
 // split-K slabs [z][split][M][N] fp32 -> sum -> epilogue (8 columns per thread)
@@ -985,6 +1030,9 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   } else {
     dispatch<T, false, true>(gg, wt, grid, kchunk, evec, sk, s);
   }
+  if (dma && g.rowsum && g.atomic && g.splitk > 1 && g.ws)   // the bias-gradient partials of the splits
+    hipLaunchKernelGGL(rowsum_reduce_kernel, dim3(dfk_cdiv(g.M, 64)), dim3(1024), 0, s,
+                       reinterpret_cast<const float*>(g.ws), g.splitk, g.M, g.rowsum);
   if (slab && !sk.cnt) {   // no ticket arena: the reduce / epilogue launch combines the splits
     const long threads = (long)g.nz0 * g.nz1 * g.M * dfk_cdiv(g.N, 8);
     hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3((unsigned)dfk_cdiv(threads, 256)), dim3(256), 0, s, g, slab,
@@ -1239,6 +1287,11 @@ uint32_t* dfk_ticket_slice(long n, hipStream_t s) {
   // profiles/gemm/r4o_inlaunch_combine_rejected.txt)
   const char* env = getenv("DFK_INLAUNCH_COMBINE");   // read per call: tests switch it inside one process
   if (!env || atoi(env) == 0 || n <= 0 || n > kTickets) return nullptr;
+  // never inside a graph capture: a slice baked into a graph stays in use at every replay, and the round-robin
+  // cursor would later hand it to another launch (two launches miscounting one slice's arrivals); captured
+  // launches take the separate combine launch instead
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
   static std::mutex mu;
   static uint32_t* arena[64] = {};
   static long cursor[64] = {};
@@ -1246,8 +1299,6 @@ uint32_t* dfk_ticket_slice(long n, hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   if (!arena[dev]) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
     void* p = nullptr;
     if (hipMalloc(&p, kTickets * 4) != hipSuccess) return nullptr;
     if (hipMemsetAsync(p, 0, kTickets * 4, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
@@ -1271,6 +1322,8 @@ extern "C" int64_t dfk_gemm_workspace(const dfk_gemm_args* g) {
   if (!g) return -1;
   const int autos = g->splitk > 1 && !g->atomic ? g->splitk
                     : (g->dtype == DFK_BF16 ? auto_splitk<bf16raw>(*g) : auto_splitk<float>(*g));
+  if (g->rowsum && g->atomic && g->splitk > 1)   // per-split bias-gradient partials (gemm_dma_kernel RS)
+    return (int64_t)g->splitk * g->M * 4;
   if (autos <= 1) return 0;
   return (int64_t)autos * g->nz0 * g->nz1 * g->M * g->N * 4;
 }

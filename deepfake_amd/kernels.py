@@ -177,7 +177,8 @@ def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None, residual=No
 _DW_MIN_K = int(os.environ.get("DFK_DW_MINK", "512"))   # tokens per split of a weight-gradient GEMM (tuning)
 _DW_UNSPLIT64 = int(os.environ.get("DFK_DW_UNSPLIT64", "384"))   # 64x64 tiles from which dW runs unsplit (r5o: the
 # 256-tile SwinV2 stage-3 fc1 / fc2 dW 22 -> 19, 21 -> 19 us on split 128x128 tiles; w2v (432-576 tiles) flat)
-_DW_XCD = int(os.environ.get("DFK_DW_XCD", "1"))   # split counts rounded to multiples of 8 (XCD grouping; A/B knob)
+_DW_XCD = int(os.environ.get("DFK_DW_XCD", "1"))
+_DW_SLAB = os.environ.get("DFK_DW_SLAB", "0") == "1"   # split counts rounded to multiples of 8 (XCD grouping; A/B knob)
 
 
 def splitk_for(tiles, K, min_k=None):
@@ -202,8 +203,9 @@ def linear_dw(dy, x, dw, db=None):
     s = max(1, min(s, max(8, M * (N + K) // (8 * N * K))))
     if _DW_XCD and tiles > 1 and s >= 16:
         s -= s % 8   # a multiple of 8 splits: the kernel puts each split's tiles on one XCD (shared operand in L2)
+    slab = s > 1 and _DW_SLAB   # A/B: fp32 split slabs + one reduce pass instead of the splits' fp32 atomics
     gemm(dy, dy.stride(0), True, x, x.stride(0), True, N, K, M, dw, dw.stride(0), dtype=L.dt(dy), c_f32=True,
-         atomic=s > 1, beta=1.0, splitk=s, rowsum=db)
+         atomic=s > 1 and not slab, beta=1.0, splitk=s, rowsum=db)
     return dw
 
 
