@@ -735,7 +735,9 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm
     // atomic split-K (the workspace holds [splitk][M] partials): one plain store per (split, row), summed by
     // rowsum_reduce_kernel — the splits' same-address atomics on the few cache lines of the bias gradient
     // serialised (stage-1 dW + db 120 -> 137 us, proj 41 -> 66 us)
-    float* rsp = g.atomic && g.splitk > 1 && g.ws ? reinterpret_cast<float*>(g.ws) + (long)split * g.M : nullptr;
+    float* rsp = g.splitk > 1 && g.ws ? reinterpret_cast<float*>(g.ws) + (g.atomic ? 0L : (long)g.splitk * g.M * g.N) +
+                                             (long)split * g.M
+                                       : nullptr;
 #pragma unroll
     for (int h = 0; h < MH; ++h) {
       const int mi = h * NWN + wn;
@@ -778,6 +780,36 @@ __global__ __launch_bounds__(1024) void rowsum_reduce_kernel(const float* __rest
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += red[i][c];
     rowsum[row] += t;
+  }
+}
+
+// fp32 C (+)= the sum of many split slabs (the weight gradients' split-K when not atomic): 64 threads x 4
+// columns per workgroup row segment, 8 split phases (each thread sums every 8th split), folded in LDS
+__global__ __launch_bounds__(512) void slab_sum_f32_kernel(const dfk_gemm_args g, const float* __restrict__ slab,
+                                                           int splitk) {
+  __shared__ f32x4 red[8][64];
+  const int c = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const long MN = (long)g.M * g.N;
+  const long i = ((long)blockIdx.x * 64 + c) * 4;   // element index in [M][N] (N % 4 == 0)
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b2 = {0.f, 0.f, 0.f, 0.f};
+  if (i < MN) {
+    int sp = ph;
+    for (; sp + 8 < splitk; sp += 16) {
+      a += *reinterpret_cast<const f32x4*>(slab + (long)sp * MN + i);
+      b2 += *reinterpret_cast<const f32x4*>(slab + (long)(sp + 8) * MN + i);
+    }
+    if (sp < splitk) a += *reinterpret_cast<const f32x4*>(slab + (long)sp * MN + i);
+  }
+  red[ph][c] = a + b2;
+  __syncthreads();
+  if (ph == 0 && i < MN) {
+    f32x4 t = red[0][c];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) t += red[k][c];
+    const long row = i / g.N, col = i % g.N;
+    float* C = reinterpret_cast<float*>(g.c) + row * g.ldc + col;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) C[e] = g.beta != 0.f ? t[e] + g.beta * C[e] : t[e];
   }
 }
 
@@ -1030,10 +1062,15 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   } else {
     dispatch<T, false, true>(gg, wt, grid, kchunk, evec, sk, s);
   }
-  if (dma && g.rowsum && g.atomic && g.splitk > 1 && g.ws)   // the bias-gradient partials of the splits
+  if (dma && g.rowsum && gg.splitk > 1 && g.ws)   // the bias-gradient partials of the splits (after the slab, if any)
     hipLaunchKernelGGL(rowsum_reduce_kernel, dim3(dfk_cdiv(g.M, 64)), dim3(1024), 0, s,
-                       reinterpret_cast<const float*>(g.ws), g.splitk, g.M, g.rowsum);
-  if (slab && !sk.cnt) {   // no ticket arena: the reduce / epilogue launch combines the splits
+                       reinterpret_cast<const float*>(g.ws) + (g.atomic ? 0L : (long)gg.splitk * g.M * g.N), gg.splitk,
+                       g.M, g.rowsum);
+  if (slab && !sk.cnt && g.c_f32 && autos >= 8 && g.N % 4 == 0 && g.nz0 == 1 && g.nz1 == 1 && !g.bias &&
+      !g.residual && !g.act) {   // many fp32 splits (weight gradients): the split loop spread over 8 phases
+    hipLaunchKernelGGL(slab_sum_f32_kernel, dim3((unsigned)dfk_cdiv((long)g.M * g.N, 256)), dim3(512), 0, s, g,
+                       slab, autos);
+  } else if (slab && !sk.cnt) {   // no ticket arena: the reduce / epilogue launch combines the splits
     const long threads = (long)g.nz0 * g.nz1 * g.M * dfk_cdiv(g.N, 8);
     hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3((unsigned)dfk_cdiv(threads, 256)), dim3(256), 0, s, g, slab,
                        autos, evec ? 1 : 0);
@@ -1322,10 +1359,11 @@ extern "C" int64_t dfk_gemm_workspace(const dfk_gemm_args* g) {
   if (!g) return -1;
   const int autos = g->splitk > 1 && !g->atomic ? g->splitk
                     : (g->dtype == DFK_BF16 ? auto_splitk<bf16raw>(*g) : auto_splitk<float>(*g));
-  if (g->rowsum && g->atomic && g->splitk > 1)   // per-split bias-gradient partials (gemm_dma_kernel RS)
-    return (int64_t)g->splitk * g->M * 4;
-  if (autos <= 1) return 0;
-  return (int64_t)autos * g->nz0 * g->nz1 * g->M * g->N * 4;
+  // per-split bias-gradient partials (gemm_dma_kernel RS), after the split slabs if there are any
+  const int64_t rs = g->rowsum && g->atomic && g->splitk > 1 ? (int64_t)g->splitk * g->M * 4
+                     : (g->rowsum && autos > 1 ? (int64_t)autos * g->M * 4 : 0);
+  if (autos <= 1) return rs;
+  return (int64_t)autos * g->nz0 * g->nz1 * g->M * g->N * 4 + rs;
 }
 
 extern "C" int dfk_colsum(const void* x, int dtype, int64_t rows, int64_t cols, int64_t ld, float* out,
