@@ -2986,8 +2986,14 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
         const uint2 x2 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 8));
         const uint2 x3 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 12));
         bf16raw* gp = dsu + (long)(kb * 32 + kr) * Np + q0 + qr0 + half * 16;
+#ifdef DFK_DS_NT
+        typedef unsigned int u32x4n __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u32x4n{x0.x, x0.y, x1.x, x1.y}, reinterpret_cast<u32x4n*>(gp));
+        __builtin_nontemporal_store(u32x4n{x2.x, x2.y, x3.x, x3.y}, reinterpret_cast<u32x4n*>(gp + 8));
+#else
         *reinterpret_cast<uint4*>(gp) = make_uint4(x0.x, x0.y, x1.x, x1.y);
         *reinterpret_cast<uint4*>(gp + 8) = make_uint4(x2.x, x2.y, x3.x, x3.y);
+#endif
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before the next step's writes
       __builtin_amdgcn_wave_barrier();
@@ -3080,12 +3086,23 @@ __global__ __launch_bounds__(256) void drpb_from_ds_kernel(const bf16raw* __rest
     const bf16raw* src = ds + (w0 * heads + h) * NN + e0;
     const long wstride = (long)heads * NN;
     long w = w0;
-    for (; w + 8 <= w1; w += 8, src += 8 * wstride) {   // eight independent 16-B loads in flight per thread
-      uint4 v[8];
+#ifndef DFK_DRPB_IF
+#define DFK_DRPB_IF 8
+#endif
+    constexpr int IF = DFK_DRPB_IF;   // independent 16-B loads in flight per thread
+    for (; w + IF <= w1; w += IF, src += IF * wstride) {
+      uint4 v[IF];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(src + u * wstride);
+      for (int u = 0; u < IF; ++u) {
+#ifndef DFK_DRPB_TEMPORAL   // streamed once: non-temporal (r5z: stage-1 backward with dRPB 934 -> 892 us, stage 3 250 -> 207)
+        typedef unsigned int u32x4n __attribute__((ext_vector_type(4)));
+        v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(src + u * wstride)));
+#else
+        v[u] = *reinterpret_cast<const uint4*>(src + u * wstride);
+#endif
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < IF; ++u) {
         const bf16raw* pe = reinterpret_cast<const bf16raw*>(&v[u]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += bf2f(pe[j]);
