@@ -617,6 +617,10 @@ __host__ __device__ __forceinline__ long view_extent(const dfk_view& v, long row
 // Workgroup tile (NWM * 64/... ) = BM x BN from NWM x NWN waves of WT x WT each: 64x64 (2x2 waves of 32),
 // 128x128 (2x2 waves of 64) and 256x128 (4x2 waves of 64, 512 threads: twice the MFMA work per k-tile for
 // 1.5x the staged bytes, so one DMA in flight covers more of its latency).
+// splits from which a dW's fused bias gradient goes through per-split partials + rowsum_reduce_kernel instead of
+// atomics (the same-address atomics serialise only when many splits add; below this, one more launch costs more)
+constexpr int kRsPartialMin = 32;
+
 template <int WT, int NWM, int NWN, bool AK, bool BKM, int S, bool RS, bool CONV = false>
 __global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm_args g, int kchunk, int evec,
                                                                   SplitK sk) {
@@ -735,9 +739,9 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_dma_kernel(const dfk_gemm
     // atomic split-K (the workspace holds [splitk][M] partials): one plain store per (split, row), summed by
     // rowsum_reduce_kernel — the splits' same-address atomics on the few cache lines of the bias gradient
     // serialised (stage-1 dW + db 120 -> 137 us, proj 41 -> 66 us)
-    float* rsp = g.splitk > 1 && g.ws ? reinterpret_cast<float*>(g.ws) + (g.atomic ? 0L : (long)g.splitk * g.M * g.N) +
-                                             (long)split * g.M
-                                       : nullptr;
+    float* rsp = g.splitk >= kRsPartialMin && g.ws
+                     ? reinterpret_cast<float*>(g.ws) + (g.atomic ? 0L : (long)g.splitk * g.M * g.N) + (long)split * g.M
+                     : nullptr;
 #pragma unroll
     for (int h = 0; h < MH; ++h) {
       const int mi = h * NWN + wn;
@@ -1062,7 +1066,7 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   } else {
     dispatch<T, false, true>(gg, wt, grid, kchunk, evec, sk, s);
   }
-  if (dma && g.rowsum && gg.splitk > 1 && g.ws)   // the bias-gradient partials of the splits (after the slab, if any)
+  if (dma && g.rowsum && gg.splitk >= kRsPartialMin && g.ws)   // the bias-gradient partials (after the slab, if any)
     hipLaunchKernelGGL(rowsum_reduce_kernel, dim3(dfk_cdiv(g.M, 64)), dim3(1024), 0, s,
                        reinterpret_cast<const float*>(g.ws) + (g.atomic ? 0L : (long)gg.splitk * g.M * g.N), gg.splitk,
                        g.M, g.rowsum);
@@ -1360,8 +1364,8 @@ extern "C" int64_t dfk_gemm_workspace(const dfk_gemm_args* g) {
   const int autos = g->splitk > 1 && !g->atomic ? g->splitk
                     : (g->dtype == DFK_BF16 ? auto_splitk<bf16raw>(*g) : auto_splitk<float>(*g));
   // per-split bias-gradient partials (gemm_dma_kernel RS), after the split slabs if there are any
-  const int64_t rs = g->rowsum && g->atomic && g->splitk > 1 ? (int64_t)g->splitk * g->M * 4
-                     : (g->rowsum && autos > 1 ? (int64_t)autos * g->M * 4 : 0);
+  const int64_t rs = g->rowsum && g->atomic && g->splitk >= kRsPartialMin ? (int64_t)g->splitk * g->M * 4
+                     : (g->rowsum && autos >= kRsPartialMin ? (int64_t)autos * g->M * 4 : 0);
   if (autos <= 1) return rs;
   return (int64_t)autos * g->nz0 * g->nz1 * g->M * g->N * 4 + rs;
 }
