@@ -678,12 +678,14 @@ __device__ __forceinline__ float grp_max4(float v) {
 //        for: mel1 backward 30 -> 25 us, the 392-token windows unchanged)
 constexpr float kPadKey = -1.0e4f;
 
+struct ClsMap { int c[8]; };   // the shift classes that occur (the grid's y covers only these)
+
 __global__ __launch_bounds__(256) void wattn_tab3_kernel(const dfk_wattn_args a, const Geo g, bf16raw* __restrict__ tf,
-                                                         bf16raw* __restrict__ tb, int fwd16) {
+                                                         bf16raw* __restrict__ tb, int fwd16, const ClsMap cm) {
   extern __shared__ int tsm[];
   int* tok = tsm;                                          // [Np]
   float* rp = reinterpret_cast<float*>(tsm + g.Np);        // [L]
-  const int ch = dfk_bid_y(), h = ch % a.heads, cls = ch / a.heads;
+  const int h = dfk_bid_y() % a.heads, cls = cm.c[dfk_bid_y() / a.heads], ch = cls * a.heads + h;
   const float pen = -100.f * kLog2e;
   for (int i = dfk_tid(); i < g.Np; i += dfk_bdim()) tok[i] = i < g.N ? tab_token(a, i) : 0;
   for (int l = dfk_tid(); l < g.L; l += dfk_bdim()) rp[l] = a.rpb ? a.rpb[(long)l * a.heads + h] * kLog2e : 0.f;
@@ -2015,9 +2017,25 @@ extern "C" int dfk_wattn_table(const dfk_wattn_args* ap, hipStream_t s) {
   const Geo g = make_geo(a);
   const TabGeo tg = tab_geo(a, g);
   bf16raw* t3 = tab3_fwd(a, g);
-  hipLaunchKernelGGL(wattn_tab3_kernel, dim3((unsigned)std::min<long>(dfk_cdiv(2 * tg.per_ch / 8, 256), 64),
-                                             tg.ncls * a.heads),
-                     dim3(256), 4 * (size_t)(g.Np + g.L), s, a, g, t3, t3 + tab_elems(a, g), fwd16_layout(a, g) ? 1 : 0);
+  // only the classes some window has (a class bit needs its dim shifted; the D-only shift of the Swin-T stage 4
+  // uses 2 of the 8): the 192-channel stage-4 table took 125 us for 384 window-heads
+  ClsMap cm{};
+  int nc = 0;
+  for (int c = 0; c < tg.ncls; ++c) {
+    const long nd = !g.use_mask ? g.nwd : ((c & 4) ? (a.sd > 0) : g.nwd - (a.sd > 0));
+    const long nh = !g.use_mask ? g.nwh : ((c & 2) ? (a.sh > 0) : g.nwh - (a.sh > 0));
+    const long nw = !g.use_mask ? g.nww : ((c & 1) ? (a.sw > 0) : g.nww - (a.sw > 0));
+    if (nd * nh * nw > 0) cm.c[nc++] = c;
+  }
+  if (nc == 0) return 0;
+  // about eight 16-B slots per thread (the per-workgroup prologue — token labels, the head's RPB column —
+  // amortised), unless that leaves fewer than 1024 workgroups (the small SwinV2 tables)
+  const long slots2 = 2 * tg.per_ch / 8;
+  long gx = std::min<long>(dfk_cdiv(slots2, 256 * 8), 64);
+  if (gx * nc * a.heads < 1024) gx = std::min<long>(dfk_cdiv(slots2, 256), std::max<long>(gx, dfk_cdiv(1024, nc * a.heads)));
+  hipLaunchKernelGGL(wattn_tab3_kernel, dim3((unsigned)gx, nc * a.heads),
+                     dim3(256), 4 * (size_t)(g.Np + g.L), s, a, g, t3, t3 + tab_elems(a, g), fwd16_layout(a, g) ? 1 : 0,
+                     cm);
   DFK_CHECK_LAUNCH();
   return 0;
 }

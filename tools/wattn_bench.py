@@ -19,6 +19,7 @@ SHAPES = [
     ("vst2 SW", (B, 16, 28, 28), (8, 7, 7), (8, 7, 7), (4, 3, 3), 6, 32, True),
     ("vst3 SW", (B, 16, 14, 14), (8, 7, 7), (8, 7, 7), (4, 3, 3), 12, 32, True),
     ("vst4 W", (B, 16, 7, 7), (8, 7, 7), (8, 7, 7), (0, 0, 0), 24, 32, True),
+    ("vst4 SWd", (B, 16, 7, 7), (8, 7, 7), (8, 7, 7), (4, 0, 0), 24, 32, True),
     ("mel1 SW", (B, 1, 56, 56), (1, 7, 7), (1, 7, 7), (0, 3, 3), 4, 32, True),
     ("w2v", (B, 1, 1, 199), (1, 1, 199), (1, 1, 199), (0, 0, 0), 12, 64, False),
 ]
@@ -63,11 +64,13 @@ def main():
         tb0 = timed(lambda: K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, 3 * C, dims, win, fw, shift, heads,
                                          hd, scale, rpb, None), dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C,
                                         drpb=None, tab=tab)) if rpb is not None else float("nan")
+        tt = timed(lambda: K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, win, fw, shift, heads, hd, scale,
+                                       rpb=rpb, out=out)) - tf if rpb is not None else float("nan")   # + the table build
         units = dims[0] * nW * heads
         ff = 4.0 * units * N * N * hd
         fb = 10.0 * units * N * N * hd
         print(f"{name:8s} units {units:6d} N {N:4d} fwd {tf:8.1f} us {ff / tf / 1e6:7.1f} TF/s | "
-              f"bwd {tb:8.1f} us {fb / tb / 1e6:7.1f} TF/s (no dRPB {tb0:7.1f} us)", flush=True)
+              f"bwd {tb:8.1f} us {fb / tb / 1e6:7.1f} TF/s (no dRPB {tb0:7.1f} us) | table {tt:6.1f} us", flush=True)
 
 
 if __name__ == "__main__":
