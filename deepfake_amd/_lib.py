@@ -140,6 +140,7 @@ SIGNATURES = {
     "dfk_frame_augment": [_VP, _I64, C.POINTER(PilResize), _VP, _VP, C.POINTER(C.c_float), C.POINTER(C.c_float),
                           _VP, _VP, _VP],
     "dfk_layerdrop_flags": [C.POINTER(Drop), _I32, _VP, _VP, _VP],
+    "dfk_layer_select": [_VP, _VP, _VP, _VP, _VP, C.c_int64, _VP],
     "dfk_spec_augment_fwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _F, _I32, _I32, C.POINTER(Drop), C.c_int, _VP],
     "dfk_spec_augment_bwd": [_VP, _VP, _VP, _VP, _I32, _I32, _I32, C.c_int, _VP],
     "dfk_frame_normalize": [_VP, _VP, _I64, _I32, _I32, C.POINTER(C.c_float), C.POINTER(C.c_float), _VP],

@@ -170,6 +170,37 @@ extern "C" int dfk_layerdrop_flags(const dfk_drop* d, int32_t n, float* keep, fl
   return 0;
 }
 
+// LayerDrop output select (forward): out = keep > 0 ? y : x, and its backward in the same form: gy = keep > 0 ? g : 0,
+// gx = keep > 0 ? 0 : g (x's other gradient is added by the caller); 16-B vectors, one launch each way
+__global__ __launch_bounds__(256) void layer_select_kernel(const uint4* __restrict__ y, const uint4* __restrict__ x,
+                                                           const float* __restrict__ keep, uint4* __restrict__ out,
+                                                           uint4* __restrict__ out2, long nv) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nv) return;
+  const bool k = *keep > 0.f;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  if (out2) {   // backward: y = g
+    const uint4 g = y[i];
+    out[i] = k ? g : z;
+    out2[i] = k ? z : g;
+  } else {
+    out[i] = k ? y[i] : x[i];
+  }
+}
+
+extern "C" int dfk_layer_select(const void* y, const void* x, const float* keep, void* out, void* out2,
+                                int64_t nbytes, hipStream_t s) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!y || !keep || !out || (!out2 && !x) || nbytes % 16 || !al(y) || !al(out) || (x && !al(x)) || (out2 && !al(out2)))
+    return DFK_EINVAL;
+  const long nv = nbytes / 16;
+  if (nv <= 0) return 0;
+  hipLaunchKernelGGL(layer_select_kernel, dim3((unsigned)dfk_cdiv(nv, 256)), dim3(256), 0, s, (const uint4*)y,
+                     (const uint4*)x, keep, (uint4*)out, (uint4*)out2, nv);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int dfk_spec_augment_fwd(const void* h, void* out, uint8_t* mask, const void* embed, int32_t B, int32_t T,
                                     int32_t C, float mask_prob, int32_t mask_length, int32_t min_masks,
                                     const dfk_drop* d, int dtype, hipStream_t s) {

@@ -431,6 +431,22 @@ class DropoutFn(torch.autograd.Function):
         return K.dropout(dy.contiguous(), ctx.drop), None
 
 
+class LayerSelectFn(torch.autograd.Function):
+    """LayerDrop (HF wav2vec2 encoder :700-706): out = y when the layer's device coin kept it, else its input x —
+    one select launch forward and one backward (torch.where took a compare, the select, two fills and two selects)."""
+
+    @staticmethod
+    def forward(ctx, y, x, keep):
+        ctx.save_for_backward(keep)
+        return K.layer_select(y.contiguous(), x.contiguous(), keep)
+
+    @staticmethod
+    def backward(ctx, g):
+        (keep,) = ctx.saved_tensors
+        gy, gx = K.layer_select_bwd(g.contiguous(), keep)
+        return gy, gx, None
+
+
 class SpecAugmentFn(torch.autograd.Function):
     """HF Wav2Vec2Model._mask_hidden_states time masking (:1272-1317): masked frames <- masked_spec_embed."""
 

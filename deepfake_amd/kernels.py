@@ -229,6 +229,11 @@ def layernorm_fwd(x, w, b, eps=1e-5, out=None, residual=None, drop=None):
     return out, mean, rstd
 
 
+# LayerNorms of <= 4096 rows: at most _LN_SMALL workgroups with atomic dw/db partials (layernorm.hip bwd_blocks)
+_LN_SMALL = int(os.environ.get("DFK_LN_SMALL", "128"))
+_LN_SMALL_ROWS = 4096
+
+
 def _ln_bwd_blocks(rows, C):
     """Workgroups of ln_bwd (layernorm.hip bwd_blocks)."""
     nv = C // 8
@@ -247,7 +252,7 @@ def layernorm_bwd(dy, x, w, mean, rstd, dw, db, dx=None, accumulate=False, slab_
     if dx is None:
         dx = torch.empty_like(x)
     if slab_partials is None:
-        slab_partials = _ln_bwd_blocks(rows, C) >= 64
+        slab_partials = _ln_bwd_blocks(rows, C) >= 64 and not (_LN_SMALL > 0 and rows <= _LN_SMALL_ROWS)
     ws = None
     if slab_partials and (dw is not None or db is not None):   # per-workgroup dw/db partials + column sums
         ws = torch.empty(max(L.lib().dfk_layernorm_bwd_workspace(rows, C) // 4, 1), device=x.device,
@@ -520,6 +525,23 @@ def bernoulli_flags(drop, n, device):
     out = torch.empty(n, device=device, dtype=torch.float32)
     L.check(L.lib().dfk_bernoulli_flags(L.drop(drop, device), n, L.ptr(out), L.stream()), "bernoulli_flags")
     return out
+
+
+def layer_select(y, x, keep, out=None):
+    """out = y if keep[0] > 0 else x (device flag, no host sync)."""
+    if out is None:
+        out = torch.empty_like(y)
+    L.check(L.lib().dfk_layer_select(L.ptr(y), L.ptr(x), L.ptr(keep), L.ptr(out), None, y.numel() * y.element_size(),
+                                     L.stream()), "layer_select")
+    return out
+
+
+def layer_select_bwd(g, keep):
+    """(the layer's gradient, the skip path's gradient) of layer_select."""
+    gy, gx = torch.empty_like(g), torch.empty_like(g)
+    L.check(L.lib().dfk_layer_select(L.ptr(g), None, L.ptr(keep), L.ptr(gy), L.ptr(gx), g.numel() * g.element_size(),
+                                     L.stream()), "layer_select_bwd")
+    return gy, gx
 
 
 def layerdrop_flags(drop, keep, used):

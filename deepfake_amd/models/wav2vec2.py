@@ -253,7 +253,12 @@ class Wav2Vec2Encoder(nn.Module):
             K.layerdrop_flags(self.layerdrop.spec(), self.layer_keep, self.layer_used)
         for i, layer in enumerate(self.layers):
             y = layer(x, B, T)
-            x = torch.where(self.layer_keep[i] > 0, y, x) if lds else y
+            if not lds:
+                x = y
+            elif x.is_cuda and y.dtype == x.dtype and (y.numel() * y.element_size()) % 16 == 0:
+                x = Fn.LayerSelectFn.apply(y, x, self.layer_keep[i:i + 1])
+            else:
+                x = torch.where(self.layer_keep[i] > 0, y, x)
         return x.view(B, T, C)
 
 

@@ -361,6 +361,12 @@ int dfk_bernoulli_flags(const dfk_drop* drop, int32_t n, float* out, hipStream_t
  * gradients): torch's SGD steps a parameter whose accumulated .grad is not None, i.e. whose layer ran in ANY
  * micro-step of the window (src/trainer.py:280-297 with HF :700-706). */
 int dfk_layerdrop_flags(const dfk_drop* drop, int32_t n, float* keep, float* used, hipStream_t stream);
+/* LayerDrop output select (HF wav2vec2 encoder :700-706, the skipped layer returns its input):
+ * forward (out2 == NULL): out = *keep > 0 ? y : x; backward (x == NULL, y = the output gradient):
+ * out = *keep > 0 ? y : 0 (the layer's), out2 = *keep > 0 ? 0 : y (the skip path's).  nbytes % 16 == 0,
+ * 16-B aligned buffers. */
+int dfk_layer_select(const void* y, const void* x, const float* keep, void* out, void* out2, int64_t nbytes,
+                     hipStream_t stream);
 /* SpecAugment time masking (HF Wav2Vec2Model._mask_hidden_states :1272-1317 with _compute_mask_indices
  * :101-218, no attention mask): per clip, num = max(min_masks, int(mask_prob*T/mask_length + eps)) (eps one
  * uniform draw per call, num clamped as HF does) distinct span starts drawn uniformly from [0, T-mask_length],

@@ -208,6 +208,26 @@ def test_layerdrop_flags_and_sgd_gate():
     assert rel(p, p0 - 0.1 * (gr + 0.05 * p0)) < 1e-6
 
 
+@pytest.mark.parametrize("kept", [0.0, 1.0])
+def test_layer_select_matches_where(kept):
+    """The fused LayerDrop select (wav2vec2 encoder: a dropped layer returns its input) against torch.where,
+    forward and both gradients, for a kept and a dropped layer (device flag)."""
+    from deepfake_amd import functional as Fn
+    g = torch.Generator(device=DEV).manual_seed(3)
+    y = torch.randn(1592, 768, device=DEV, generator=g).to(torch.bfloat16).requires_grad_(True)
+    x = torch.randn(1592, 768, device=DEV, generator=g).to(torch.bfloat16).requires_grad_(True)
+    keep = torch.full((1,), kept, device=DEV)
+    dout = torch.randn(1592, 768, device=DEV, generator=g).to(torch.bfloat16)
+    out = Fn.LayerSelectFn.apply(y, x, keep)
+    out.backward(dout)
+    gy, gx = y.grad.clone(), x.grad.clone()
+    y.grad = x.grad = None
+    ref = torch.where(keep[0] > 0, y, x)
+    ref.backward(dout)
+    assert torch.equal(out, ref)
+    assert torch.equal(gy, y.grad) and torch.equal(gx, x.grad)
+
+
 @pytest.mark.parametrize("world", [3, 4])
 def test_sgd_data_parallel_fold(world):
     """The fused step consumes the all-reduced SUM: grad_scale = 1 / world replaces the averaging pass, and
