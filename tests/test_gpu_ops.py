@@ -119,6 +119,25 @@ def test_linear_dw_token_streaming(M, N, Kd, monkeypatch):
     assert rel(dw2, dy.double().t() @ x.double()) < 1e-4
 
 
+@pytest.mark.parametrize("slab", [False, True])
+@pytest.mark.parametrize("M,N,Kd", [(50176, 96, 96), (40000, 384, 96), (1568, 2048, 512), (1592, 768, 3072)])
+def test_linear_dw_bias_partials(M, N, Kd, slab, monkeypatch):
+    """The weight gradient with its fused bias gradient on every split path: >= 32 atomic splits (the stage-1
+    shapes: per-split bias partials + rowsum_reduce_kernel), few atomic splits (bias atomics), unsplit, and the fp32
+    split-slab path (kernels._DW_SLAB: slab_sum_f32_kernel, bias partials after the slab) — against fp64, into
+    non-zero dW / db."""
+    monkeypatch.setattr(K, "_DW_SLAB", slab)
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.randn(M, Kd, device=DEV, generator=g).to(torch.bfloat16)
+    dy = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    dw0 = torch.randn(N, Kd, device=DEV, generator=g)
+    db0 = torch.randn(N, device=DEV, generator=g)
+    dw, db = dw0.clone(), db0.clone()
+    K.linear_dw(dy, x, dw, db=db)
+    assert rel(dw, dw0.double() + dy.double().t() @ x.double()) < 1e-4
+    assert rel(db, db0.double() + dy.double().sum(0)) < 1e-4
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,Kd", [(1000, 288, 96), (1568, 512, 2048), (1592, 768, 3072), (1592, 2304, 768)])
 def test_inlaunch_combine(dt, M, N, Kd, monkeypatch):
