@@ -184,26 +184,29 @@ def draw_augment(frames, generator=None, degrees=90.0):
     """Per-frame parameters of T.RandomHorizontalFlip, T.RandomVerticalFlip (p = 0.5) and T.RandomRotation(90),
     drawn on the CPU in the order the reference's Compose draws them for each frame (torch.rand(1) < 0.5,
     torch.rand(1) < 0.5, torch.empty(1).uniform_(-90, 90)): (flips int32 [frames] (bit 0 horizontal, bit 1
-    vertical), angles: list of Python floats)."""
-    flips, angles = [], []
-    for _ in range(frames):
-        hf = bool(torch.rand(1, generator=generator) < 0.5)
-        vf = bool(torch.rand(1, generator=generator) < 0.5)
-        ang = float(torch.empty(1).uniform_(-degrees, degrees, generator=generator).item())
-        flips.append(int(hf) | (int(vf) << 1))
-        angles.append(ang)
-    return torch.tensor(flips, dtype=torch.int32), angles
+    vertical), angles: list of Python floats).  One batched draw of [frames, 3] uniforms: the CPU generator
+    hands them out in the same sequence as the per-frame scalar calls, and uniform_(a, b) on one float is
+    float32(double(u) * (b - a) + a) of the same 24-bit draw, so flips, angles and the generator's state afterwards
+    are identical to the scalar loop (tests/test_media_oracle.py pins this)."""
+    u = torch.rand(frames, 3, generator=generator)
+    flips = ((u[:, 0] < 0.5).int() | ((u[:, 1] < 0.5).int() << 1)).to(torch.int32)
+    angles = (u[:, 2].double() * (2.0 * degrees) - degrees).float()
+    return flips, angles.tolist()
 
 
-def frame_augment(frames_u8, size=(224, 224), flips=None, angles=None, mean=IMAGENET_MEAN, std=IMAGENET_STD):
-    """uint8 [..., H, W, 3] decoded RGB frames (or [..., H, W] grey images) on the device -> fp32
+def frame_augment(frames_u8, size=(224, 224), flips=None, angles=None, mean=IMAGENET_MEAN, std=IMAGENET_STD,
+                  grey=False):
+    """uint8 [..., H, W, 3] decoded RGB frames (or, with grey=True, [..., H, W] grey images) on the device -> fp32
     [..., 3, size[1], size[0]]: PIL Resize, flips, rotation, ToTensor, Normalize (data_process.py:55-69 on PIL
     images).  flips: int tensor [frames] (None: none); angles: per-frame rotation angles in degrees (host floats,
     None: none)."""
     x = frames_u8
     if x.dtype != torch.uint8:
         raise ValueError("frame_augment expects uint8 frames")
-    grey = x.shape[-1] != 3
+    if grey and x.dim() < 2:
+        raise ValueError("grey frame_augment expects [..., H, W]")
+    if not grey and (x.dim() < 3 or x.shape[-1] != 3):
+        raise ValueError("frame_augment expects RGB frames [..., H, W, 3] (grey=True for [..., H, W])")
     *lead, H, W = (x.shape if grey else x.shape[:-1])
     cin = 1 if grey else 3
     x = x.contiguous()

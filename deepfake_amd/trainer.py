@@ -105,7 +105,7 @@ def prepare_mel(audio, device, augment=False, generator=None, size=224):
         if augment:
             n = a.numel() // (a.shape[-2] * a.shape[-1])
             flips, angles = media.draw_augment(n, generator)
-            return media.frame_augment(a, (size, size), flips=flips, angles=angles)
+            return media.frame_augment(a, (size, size), flips=flips, angles=angles, grey=True)
         return media.gray_normalize(a)
     return a
 

@@ -75,7 +75,7 @@ def test_frame_augment_matches_pil(name, h, w, ch):
     aug = name != "resize720"
     flips = torch.from_numpy(fx[name + ":flips"]) if aug else None
     angles = [float(a) for a in fx[name + ":angles"]] if aug else None
-    out = media.frame_augment(src, flips=flips, angles=angles).cpu()
+    out = media.frame_augment(src, flips=flips, angles=angles, grey=ch == 1).cpu()
     ref = torch.stack([_norm(torch.from_numpy(fx[name][i]).permute(2, 0, 1)) for i in range(n)])
     assert torch.equal(out, ref), int((out != ref).any(1).sum())
 
@@ -126,7 +126,7 @@ def test_trainer_media_inputs():
     ga, gb = torch.Generator().manual_seed(5), torch.Generator().manual_seed(5)
     ma = prepare_mel(gray0, DEV, augment=True, generator=ga)
     flips, angles = media.draw_augment(2, gb)
-    assert torch.equal(ma, media.frame_augment(gray0.to(DEV), flips=flips, angles=angles))
+    assert torch.equal(ma, media.frame_augment(gray0.to(DEV), flips=flips, angles=angles, grey=True))
     assert not torch.equal(ma, media.gray_normalize(gray0.to(DEV)))
     wave = 0.1 * torch.randn(2, 22050 * 2, generator=g)
     m = prepare_mel(wave, DEV)

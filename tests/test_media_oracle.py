@@ -96,3 +96,40 @@ def test_product_pil_constants_match_oracle():
     for ang in (0.0, 37.5, -61.25, 90.0, 180.0, -89.99):
         m = media.pil_rotate_fixed(ang, 224, 224)
         assert (m[0] == 0) == (ang % 360.0 == 0)
+
+
+def _scalar_draws(frames, generator, degrees=90.0):
+    """The reference Compose's per-frame draw sequence (data_process.py:62-69): rand(1) < 0.5 twice, then
+    RandomRotation's empty(1).uniform_(-90, 90), one frame after the other."""
+    flips, angles = [], []
+    for _ in range(frames):
+        hf = bool(torch.rand(1, generator=generator) < 0.5)
+        vf = bool(torch.rand(1, generator=generator) < 0.5)
+        angles.append(float(torch.empty(1).uniform_(-degrees, degrees, generator=generator).item()))
+        flips.append(int(hf) | (int(vf) << 1))
+    return flips, angles
+
+
+def test_draw_augment_matches_scalar_draws():
+    """media.draw_augment's batched draw gives the per-frame scalar sequence bit for bit, and leaves the generator
+    where the scalar loop leaves it."""
+    from deepfake_amd import media
+    for n in (1, 2, 17, 256):
+        for seed in range(3):
+            ga, gb = torch.Generator().manual_seed(seed), torch.Generator().manual_seed(seed)
+            flips, angles = media.draw_augment(n, ga)
+            rf, ra = _scalar_draws(n, gb)
+            assert flips.dtype == torch.int32 and flips.tolist() == rf and angles == ra
+            assert torch.equal(torch.rand(4, generator=ga), torch.rand(4, generator=gb))
+
+
+def test_frame_augment_shape_contract():
+    """RGB frames must be [..., H, W, 3]; grey images are routed by grey=True, never by a shape guess."""
+    import pytest
+    from deepfake_amd import media
+    with pytest.raises(ValueError, match="RGB"):
+        media.frame_augment(torch.zeros(2, 224, 224, dtype=torch.uint8))
+    with pytest.raises(ValueError, match="RGB"):
+        media.frame_augment(torch.zeros(224, 3, dtype=torch.uint8))
+    with pytest.raises(ValueError, match="grey"):
+        media.frame_augment(torch.zeros(5, dtype=torch.uint8), grey=True)
