@@ -122,6 +122,7 @@ SIGNATURES = {
     "dfk_w2v_conv0_fwd_workspace": [_I64, _I64],
     "dfk_w2v_conv0_bwd": [_VP, _I64, _I64, _VP, _VP, _VP, _F, _VP, _VP, C.c_int, _VP, _I64, _VP, _VP, _VP, _VP],
     "dfk_w2v_conv0_bwd_workspace": [_I64, _I64],
+    "dfk_sgd_step_runs": [_VP, _VP, _VP, _VP, _VP, C.c_int32, _VP, _F, _F, _F, _F, _VP, _VP],
     "dfk_sgd_step": [_VP, _VP, _VP, _VP, _I64, _VP, _F, _F, _F, C.c_int, _VP, _F, _VP, _VP],
     "dfk_im2col2d": [_VP, _I64, _VP, C.POINTER(Conv2dGeo), C.c_int, _VP],
     "dfk_col2im2d": [_VP, _VP, _I64, C.POINTER(Conv2dGeo), C.c_int, C.c_int, _VP],

@@ -202,6 +202,90 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ grad
   }
 }
 
+// All runs of one step in one launch (dfk_sgd_step_runs): the run table travels by value in the kernel
+// arguments (no device table to keep alive across graph replays); a workgroup owns kSgdRunBlock consecutive
+// elements of one run (two float4 per thread, so each wave keeps 2x the bytes of the one-run kernel in flight).
+constexpr int kSgdRunBlock = 2048;
+constexpr int kSgdMaxRuns = 64;
+struct SgdRuns {
+  int64_t start[kSgdMaxRuns], n[kSgdMaxRuns];
+  const float* gate[kSgdMaxRuns];
+  int32_t prefix[kSgdMaxRuns + 1];    // first workgroup of each run; prefix[nruns] = the grid
+  uint64_t first;                     // bit r: run r takes its first momentum step
+  int32_t nruns;
+};
+
+__global__ __launch_bounds__(256) void sgd_runs_kernel(float* __restrict__ P, const float* __restrict__ G,
+                                                       float* __restrict__ Bf, bf16raw* __restrict__ S,
+                                                       const SgdRuns R, const float* __restrict__ lr_dev,
+                                                       float lr_host, float mom, float wd, float gscale,
+                                                       const bf16raw* __restrict__ GB) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = R.nruns - 1;                   // the run with prefix[lo] <= b < prefix[lo + 1]
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (R.prefix[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const long start = R.start[lo], n = R.n[lo];
+  const float* gate = R.gate[lo];
+  const int first = (int)((R.first >> lo) & 1);
+  if (gate && *gate == 0.f) return;
+  const float lr = lr_dev ? *lr_dev : lr_host;
+  const long base = (long)(b - R.prefix[lo]) * kSgdRunBlock;
+  float* p = P + start;
+  float* buf = Bf + start;
+  const float* grad = G + start;
+  const bf16raw* gbf = GB ? GB + start : nullptr;
+  bf16raw* shadow = S ? S + start : nullptr;
+  long idx[2] = {base + threadIdx.x * 4, base + 1024 + threadIdx.x * 4};
+  float4 pv[2], gv[2], bv[2];
+  bool full[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    full[u] = idx[u] + 4 <= n;
+    if (!full[u]) continue;
+    pv[u] = *reinterpret_cast<const float4*>(p + idx[u]);
+    if (gbf) {
+      const uint2 w = *reinterpret_cast<const uint2*>(gbf + idx[u]);
+      gv[u] = make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                          __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u));
+    } else {
+      gv[u] = *reinterpret_cast<const float4*>(grad + idx[u]);
+    }
+    bv[u] = first ? make_float4(0, 0, 0, 0) : *reinterpret_cast<const float4*>(buf + idx[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (full[u]) {
+      float* pp = reinterpret_cast<float*>(&pv[u]);
+      const float* gg = reinterpret_cast<const float*>(&gv[u]);
+      float* bb = reinterpret_cast<float*>(&bv[u]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float g = gg[k] * gscale + wd * pp[k];
+        bb[k] = first ? g : mom * bb[k] + g;
+        pp[k] -= lr * bb[k];
+      }
+      *reinterpret_cast<float4*>(p + idx[u]) = pv[u];
+      *reinterpret_cast<float4*>(buf + idx[u]) = bv[u];
+      if (shadow) {
+        uint2 w;
+        bf16raw* e = reinterpret_cast<bf16raw*>(&w);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = f2bf(pp[k]);
+        *reinterpret_cast<uint2*>(shadow + idx[u]) = w;
+      }
+    } else {
+      for (long i = idx[u]; i < n; ++i) {        // the run's last < 4 elements
+        const float g = (gbf ? bf2f(gbf[i]) : grad[i]) * gscale + wd * p[i];
+        buf[i] = first ? g : mom * buf[i] + g;
+        p[i] -= lr * buf[i];
+        if (shadow) shadow[i] = f2bf(p[i]);
+      }
+    }
+  }
+}
+
 // SwinV2 cosine attention prologue (swin_transformer2d.py:154-157): per (row, head)
 //   q' = q / max(|q|, 1e-12) * scale[h] ;  k' = k / max(|k|, 1e-12) ;  v' = v
 // G = hd/8 consecutive lanes per (row, head), 8 elements (16 B) of q, k and v each; the norms reduce
@@ -448,6 +532,37 @@ extern "C" int dfk_sgd_step(float* param, const float* grad, float* momentum_buf
   auto kfn = nt ? sgd_kernel<true> : sgd_kernel<false>;
   hipLaunchKernelGGL(kfn, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, param, grad, momentum_buf,
                      (bf16raw*)bf16_shadow, (long)n, lr_dev, lr, momentum, weight_decay, first_step, gate, grad_scale,
+                     (const bf16raw*)grad_bf16);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_sgd_step_runs(float* param, const float* grad, float* momentum_buf, void* bf16_shadow,
+                                 const int64_t* runs, int32_t nruns, const float* lr_dev, float lr, float momentum,
+                                 float weight_decay, float grad_scale, const void* grad_bf16, hipStream_t s) {
+  if (!param || !grad || !momentum_buf || !runs || nruns <= 0) return DFK_EINVAL;
+  if (nruns > kSgdMaxRuns) return DFK_ENOTSUP;
+  if ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
+       reinterpret_cast<uintptr_t>(momentum_buf)) & 15)
+    return DFK_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(grad_bf16) | reinterpret_cast<uintptr_t>(bf16_shadow)) & 7) return DFK_EINVAL;
+  SgdRuns R{};
+  R.nruns = nruns;
+  int64_t blocks = 0;
+  for (int r = 0; r < nruns; ++r) {
+    const int64_t* e = runs + 4 * r;          // {start, n, gate pointer, first}
+    if (e[1] <= 0 || e[0] < 0 || (e[0] & 3)) return DFK_EINVAL;
+    R.start[r] = e[0];
+    R.n[r] = e[1];
+    R.gate[r] = reinterpret_cast<const float*>(e[2]);
+    if (e[3]) R.first |= 1ull << r;
+    R.prefix[r] = (int32_t)blocks;
+    blocks += (e[1] + kSgdRunBlock - 1) / kSgdRunBlock;
+    if (blocks > 0x7fffffffL) return DFK_EINVAL;
+  }
+  R.prefix[nruns] = (int32_t)blocks;
+  hipLaunchKernelGGL(sgd_runs_kernel, dim3((unsigned)blocks), dim3(256), 0, s, param, grad, momentum_buf,
+                     (bf16raw*)bf16_shadow, R, lr_dev, lr, momentum, weight_decay, grad_scale,
                      (const bf16raw*)grad_bf16);
   DFK_CHECK_LAUNCH();
   return 0;

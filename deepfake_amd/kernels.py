@@ -4,6 +4,7 @@ Every function enqueues on torch's current HIP stream, allocates outputs with
 the torch caching allocator (graph-capture safe) and raises on any error.
 Activations are 2-D token-major views ([rows, C], contiguous rows).
 """
+import ctypes
 import math
 import os
 
@@ -508,6 +509,22 @@ def sgd_step(param, grad, buf, shadow, lr, momentum, wd, first, lr_dev=None, gat
                                  param.numel(), L.ptr(lr_dev) if lr_dev is not None else None, float(lr),
                                  float(momentum), float(wd), int(first), L.ptr(gate), float(grad_scale),
                                  L.ptr(grad_bf16) if grad_bf16 is not None else None, L.stream()), "sgd_step")
+
+
+SGD_MAX_RUNS = 64   # dfk_sgd_step_runs' by-value run table
+
+
+def sgd_step_runs(param, grad, buf, shadow, runs, momentum, wd, lr_dev, grad_scale=1.0, grad_bf16=None):
+    """Every run [(start, end, gate tensor or None, first)] of one SGD step in one launch (same per-element
+    arithmetic as sgd_step); the run table is host data copied into the launch arguments."""
+    if not 0 < len(runs) <= SGD_MAX_RUNS:
+        raise ValueError(f"sgd_step_runs takes 1..{SGD_MAX_RUNS} runs")
+    tab = (ctypes.c_int64 * (4 * len(runs)))(*[v for s, e, g, f in runs
+                                          for v in (s, e - s, g.data_ptr() if g is not None else 0, int(bool(f)))])
+    L.check(L.lib().dfk_sgd_step_runs(L.ptr(param), L.ptr(grad), L.ptr(buf), L.ptr(shadow) if shadow is not None
+                                      else None, tab, len(runs), L.ptr(lr_dev), 0.0, float(momentum), float(wd),
+                                      float(grad_scale), L.ptr(grad_bf16) if grad_bf16 is not None else None,
+                                      L.stream()), "sgd_step_runs")
 
 
 def dropout(x, drop, out=None, group_rows=None):

@@ -6,10 +6,15 @@ buffer, which also rewrites the bf16 compute shadow.  The learning rate lives
 in device memory so a captured graph replays with the scheduler's current lr.
 """
 import math
+import os
 
 import torch
 
 from . import kernels as K
+
+
+# DFK_SGD_RUNS=0: one dfk_sgd_step launch per run (A/B); default: every run in one dfk_sgd_step_runs launch
+_RUNS = os.environ.get("DFK_SGD_RUNS", "1") != "0"
 
 
 class FusedSGD:
@@ -29,7 +34,8 @@ class FusedSGD:
 
     def step(self, first=None, grad_scale=1.0, grad_bf16=None):
         """One SGD step over the parameters that received a gradient (torch skips grad=None:
-        no weight decay and no momentum for them), in as few contiguous launches as possible.
+        no weight decay and no momentum for them): every contiguous run in one dfk_sgd_step_runs launch (one
+        dfk_sgd_step per run beyond 64 runs, or with DFK_SGD_RUNS=0).
         grad_scale / grad_bf16: the data-parallel fold of GradBucketer.finish(fold=True) — the gradient is the
         all-reduced sum (in the fp32 buffer, or in the bf16 bucket copy) times 1 / world."""
         st = self.store
@@ -44,6 +50,12 @@ class FusedSGD:
                 if t:
                     self.has_buf[i] = True
         # a LayerDrop-gated run is skipped on the device when its layer was dropped this step
+        if _RUNS and 0 < len(runs) <= K.SGD_MAX_RUNS:
+            K.sgd_step_runs(st.flat, st.grad, self.buf, st.shadow, [(s, e, gates.get(k), f) for s, e, (f, k) in runs],
+                            self.momentum, self.weight_decay, self.lr_dev, grad_scale=grad_scale,
+                            grad_bf16=grad_bf16)
+            self.first = False
+            return
         for s, e, (f, k) in runs:
             K.sgd_step(st.flat[s:e], st.grad[s:e], self.buf[s:e], st.shadow[s:e] if st.shadow is not None else None,
                        0.0, self.momentum, self.weight_decay, bool(f), lr_dev=self.lr_dev, gate=gates.get(k),

@@ -25,6 +25,7 @@ extern "C" {
 #define DFK_F32 0
 #define DFK_BF16 1
 #define DFK_EINVAL (-1)
+#define DFK_ENOTSUP (-2)   /* a size the entry point does not take (documented per entry point) */
 
 /* Training-mode dropout / DropPath / LayerDrop masks, drawn by a counter-based hash inside the kernels
  * that apply them, so the backward regenerates the forward's mask and a captured HIP graph draws new
@@ -342,6 +343,14 @@ int dfk_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, int dtype
 int dfk_sgd_step(float* param, const float* grad, float* momentum_buf, void* bf16_shadow, int64_t n,
                  const float* lr_dev, float lr, float momentum, float weight_decay, int first_step,
                  const float* gate, float grad_scale, const void* grad_bf16, hipStream_t stream);
+/* Every run of one optimizer step in one launch (replaces the per-run dfk_sgd_step loop of optim.FusedSGD.step;
+ * same arithmetic per element).  runs: HOST int64 [nruns][4] = {start element, n, gate device pointer (0: none),
+ * first_step}, copied into the launch's arguments (so a captured graph holds no table pointer); nruns <= 64
+ * (DFK_ENOTSUP beyond that: the caller loops dfk_sgd_step).  Run starts are multiples of 4 elements (param / grad /
+ * momentum 16-B, grad_bf16 / shadow 8-B aligned). */
+int dfk_sgd_step_runs(float* param, const float* grad, float* momentum_buf, void* bf16_shadow, const int64_t* runs,
+                      int32_t nruns, const float* lr_dev, float lr, float momentum, float weight_decay,
+                      float grad_scale, const void* grad_bf16, hipStream_t stream);
 /* gate (above; may be NULL): device flag, the step is skipped when *gate == 0 — the parameters of a
  * LayerDrop-skipped wav2vec2 layer have grad None in the reference and torch's SGD leaves them (and
  * their momentum) untouched.

@@ -255,6 +255,34 @@ def test_sgd_data_parallel_fold(world):
             assert rel(buf, bref) < 1e-6 and rel(p, p0 - 0.1 * bref) < 1e-6
 
 
+@pytest.mark.parametrize("fold", [False, True])
+def test_sgd_runs_one_launch_matches_per_run(fold):
+    """dfk_sgd_step_runs (every run of the step in one launch, optim.FusedSGD's default) against one dfk_sgd_step
+    per run, bit for bit: ragged run lengths (scalar tails, runs shorter than a workgroup), gaps between runs left
+    untouched, a dropped (gate 0) and a kept (gate 1) LayerDrop run, first / later momentum, the bf16 shadow, and
+    the data-parallel fold (1 / world, bf16 bucket gradient)."""
+    g = torch.Generator(device=DEV).manual_seed(7)
+    n = 60000
+    p0, g0, b0 = (torch.randn(n, device=DEV, generator=g) for _ in range(3))
+    gb = (g0 * 3).to(torch.bfloat16) if fold else None
+    off, on = torch.zeros(1, device=DEV), torch.ones(1, device=DEV)
+    runs = [(0, 5003, None, True), (5008, 5012, off, False), (5016, 30000, on, False), (30008, 30009, None, False),
+            (30016, 59999, None, True)]
+    scale = 1.0 / 3 if fold else 1.0
+    pa, ba, sa = p0.clone(), b0.clone(), torch.zeros(n, device=DEV, dtype=torch.bfloat16)
+    for s, e, gate, first in runs:
+        K.sgd_step(pa[s:e], g0[s:e], ba[s:e], sa[s:e], 0.0, 0.9, 0.05, first, lr_dev=torch.full((1,), 0.1, device=DEV),
+                   gate=gate, grad_scale=scale, grad_bf16=gb[s:e] if gb is not None else None)
+    pb, bb, sb = p0.clone(), b0.clone(), torch.zeros(n, device=DEV, dtype=torch.bfloat16)
+    K.sgd_step_runs(pb, g0, bb, sb, runs, 0.9, 0.05, torch.full((1,), 0.1, device=DEV), grad_scale=scale,
+                    grad_bf16=gb)
+    torch.cuda.synchronize()
+    assert torch.equal(pa, pb) and torch.equal(ba, bb) and torch.equal(sa, sb)
+    for s, e in ((5003, 5016), (30000, 30008), (30009, 30016), (59999, n)):   # dropped run and gaps: untouched
+        assert torch.equal(pb[s:e], p0[s:e]) and torch.equal(bb[s:e], b0[s:e])
+    assert not torch.equal(pb[5016:30000], p0[5016:30000])
+
+
 def test_fused_c1_regularized_step():
     """The C1 fused model with the reference's regularisers trains (finite loss, gradients everywhere the
     reference has them), its masks change from step to step, and eval mode is the deterministic model."""
