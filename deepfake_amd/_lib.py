@@ -59,7 +59,8 @@ class WattnArgs(C.Structure):
 class WattnBwdArgs(C.Structure):
     _fields_ = [("f", WattnArgs), ("dout", C.c_void_p), ("dq", C.c_void_p), ("dk", C.c_void_p),
                 ("dv", C.c_void_p), ("drpb", C.c_void_p), ("dpad_q", C.c_void_p), ("dpad_k", C.c_void_p),
-                ("dpad_v", C.c_void_p), ("ld_dqkv", C.c_int64), ("ld_dout", C.c_int64), ("ws", C.c_void_p)]
+                ("dpad_v", C.c_void_p), ("ld_dqkv", C.c_int64), ("ld_dout", C.c_int64), ("ws", C.c_void_p),
+                ("dscore", C.c_void_p)]
 
 
 class PatchEmbedArgs(C.Structure):
@@ -113,7 +114,7 @@ SIGNATURES = {
     "dfk_cast": [_VP, C.c_int, _VP, C.c_int, _I64, _VP],
     "dfk_gelu_bwd": [_VP, _VP, _VP, _I64, C.c_int, _VP],
     "dfk_cosine_qk_fwd": [_VP, _VP, _VP, _F, _I64, C.c_int, C.c_int, C.c_int, _VP],
-    "dfk_cosine_qk_bwd": [_VP, _VP, _VP, _VP, _F, _VP, _I64, C.c_int, C.c_int, C.c_int, _VP],
+    "dfk_cosine_qk_bwd": [_VP, _VP, _VP, _VP, _F, _VP, _I64, C.c_int, C.c_int, C.c_int, _VP, _VP],
     "dfk_cpb_bias_fwd": [_VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],
     "dfk_cpb_bias_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],
     "dfk_cpb_bias_fwd_many": [_VP, _I32, _I32, _VP, _VP],

@@ -1066,7 +1066,9 @@ int launch(const dfk_gemm_args& g, hipStream_t s) {
   } else {
     dispatch<T, false, true>(gg, wt, grid, kchunk, evec, sk, s);
   }
-  if (dma && g.rowsum && gg.splitk >= kRsPartialMin && g.ws)   // the bias-gradient partials (after the slab, if any)
+  // the bias-gradient partials (after the slab, if any): only gemm_dma_kernel writes them (dma && vec); the
+  // register-staged kernels add the bias gradient atomically into rowsum and leave the workspace untouched
+  if (dma && vec && g.rowsum && gg.splitk >= kRsPartialMin && g.ws)
     hipLaunchKernelGGL(rowsum_reduce_kernel, dim3(dfk_cdiv(g.M, 64)), dim3(1024), 0, s,
                        reinterpret_cast<const float*>(g.ws) + (g.atomic ? 0L : (long)gg.splitk * g.M * g.N), gg.splitk,
                        g.M, g.rowsum);
@@ -1363,9 +1365,13 @@ extern "C" int64_t dfk_gemm_workspace(const dfk_gemm_args* g) {
   if (!g) return -1;
   const int autos = g->splitk > 1 && !g->atomic ? g->splitk
                     : (g->dtype == DFK_BF16 ? auto_splitk<bf16raw>(*g) : auto_splitk<float>(*g));
-  // per-split bias-gradient partials (gemm_dma_kernel RS), after the split slabs if there are any
-  const int64_t rs = g->rowsum && g->atomic && g->splitk >= kRsPartialMin ? (int64_t)g->splitk * g->M * 4
-                     : (g->rowsum && autos >= kRsPartialMin ? (int64_t)autos * g->M * 4 : 0);
+  // per-split bias-gradient partials (gemm_dma_kernel RS, i.e. the LDS-DMA vector path only), after the split
+  // slabs if there are any
+  const bool dmav = g->dtype == DFK_BF16 && dma_ok(*g) && view_vec(g->a, 8) && view_vec(g->b, 8) &&
+                    (g->a_kmajor ? g->M : g->K) % 8 == 0 && (g->b_kmajor ? g->N : g->K) % 8 == 0;
+  const int64_t rs = !dmav || !g->rowsum ? 0
+                     : (g->atomic && g->splitk >= kRsPartialMin ? (int64_t)g->splitk * g->M * 4
+                                                                : (autos >= kRsPartialMin ? (int64_t)autos * g->M * 4 : 0));
   if (autos <= 1) return rs;
   return (int64_t)autos * g->nz0 * g->nz1 * g->M * g->N * 4 + rs;
 }

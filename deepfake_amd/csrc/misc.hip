@@ -334,7 +334,7 @@ template <typename T, int G>
 __global__ __launch_bounds__(256) void cosine_bwd_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                          T* __restrict__ dqkv, const float* __restrict__ logit,
                                                          float max_log, float* __restrict__ dlogit, long rows,
-                                                         int heads) {
+                                                         int heads, float* __restrict__ dscore) {
   __shared__ float red[64];
   if (threadIdx.x < 64) red[threadIdx.x] = 0.f;
   __syncthreads();
@@ -374,7 +374,15 @@ __global__ __launch_bounds__(256) void cosine_bwd_kernel(const T* __restrict__ q
     float dv[8];
     ld8<T>(dout + base + 2 * C, dv);
     st8<T>(dqkv + base + 2 * C, dv);
-    if (l == 0) atomicAdd(&red[h & 63], dsq);
+    if (l == 0 && !dscore) atomicAdd(&red[h & 63], dsq);
+  }
+  if (dscore) {   // the attention backward took sum dS * score in fp32 (dfk_wattn_bwd_args.dscore): use it, re-zero it
+    if (blockIdx.x == 0 && threadIdx.x < heads) {
+      const float v = dscore[threadIdx.x];
+      dscore[threadIdx.x] = 0.f;
+      if (logit[threadIdx.x] <= max_log) atomicAdd(dlogit + threadIdx.x, v);
+    }
+    return;
   }
   __syncthreads();
   if (threadIdx.x < heads && threadIdx.x < 64 && red[threadIdx.x] != 0.f) {
@@ -402,7 +410,8 @@ extern "C" int dfk_cosine_qk_fwd(const void* qkv, void* out, const float* logit_
 }
 
 extern "C" int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, const float* logit_scale, float max_log,
-                                 float* dlogit_scale, int64_t rows, int heads, int hd, int dtype, hipStream_t s) {
+                                 float* dlogit_scale, int64_t rows, int heads, int hd, int dtype, float* dscore,
+                                 hipStream_t s) {
   if (!qkv || !dout || !dqkv || !logit_scale || !dlogit_scale || heads <= 0 || heads > 64 || (hd != 32 && hd != 64))
     return DFK_EINVAL;
   if (reinterpret_cast<uintptr_t>(qkv) % 16 || reinterpret_cast<uintptr_t>(dout) % 16 ||
@@ -412,7 +421,7 @@ extern "C" int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, 
   if (n <= 0) return 0;
   const dim3 grid((unsigned)((n + 255) / 256));
 #define COS_B(T, G) hipLaunchKernelGGL((cosine_bwd_kernel<T, G>), grid, dim3(256), 0, s, (const T*)qkv, (const T*)dout, \
-                                       (T*)dqkv, logit_scale, max_log, dlogit_scale, (long)rows, heads)
+                                       (T*)dqkv, logit_scale, max_log, dlogit_scale, (long)rows, heads, dscore)
   if (dtype == DFK_BF16) { if (hd == 32) COS_B(bf16raw, 4); else COS_B(bf16raw, 8); }
   else { if (hd == 32) COS_B(float, 4); else COS_B(float, 8); }
 #undef COS_B

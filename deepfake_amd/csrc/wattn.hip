@@ -2006,8 +2006,9 @@ static long g_fwd_bal_min = getenv("DFK_WATTN_BALMIN") ? atol(getenv("DFK_WATTN_
 // where the goldens hold them (r5j: C1 mel layers.1.blocks.1 logit_scale norm 5.7 % with v4, 8.6 % with v6, against
 // 1.1 % in the reference's own bf16 run — the same attention error, rms 2.8e-3 either way, tools/wattn_err.py, in a
 // gradient that cancels to a few % of its terms)
+static const int g_v6_min_qb = getenv("DFK_WATTN_V6MIN") ? atoi(getenv("DFK_WATTN_V6MIN")) : 4;   // A/B runs only
 static bool use_v6(const dfk_wattn_args& a, const Geo& g) {
-  return g_fwd_version == 6 && a.hd == 32 && !a.drop.mode && g.Np / 32 >= 4;
+  return g_fwd_version == 6 && a.hd == 32 && !a.drop.mode && g.Np / 32 >= g_v6_min_qb;
 }
 static bool fwd16_layout(const dfk_wattn_args& a, const Geo& g) { return use_v6(a, g); }
 
@@ -2774,13 +2775,37 @@ __global__ __launch_bounds__(HD == 32 ? 512 : 256) void wattn_bwd_bf16_kernel(co
 //   dV^T += dO^T P, dK^T += Q'^T dS  (the score accumulators are the B operands: no lane movement)
 //   dQ_part = dS K              (dS crosses the wave's LDS scratch once, as dS^T, read back transposed)
 // dS^T also goes to the global scratch (dsg) for the deterministic dRPB reduction.
+// COS (SwinV2 cosine attention, ba.dscore): the gradient of a per-head multiplier of the scores (logit_scale,
+// swin_transformer2d.py:155-157), dscore[h] += sum_q sum_k dS ⊙ score — in fp32 from the fp32 P, dP and score the
+// loop already holds, with the softmax-backward row constant taken exactly: per row, A' = sum_k P (dP - delta) r,
+// D' = sum_k P (dP - delta), B = sum_k P r (r = the score before bias, sum_k P = 1), so sum_k dS r with the exact
+// delta = sum_k P dP is A' - D' B whatever the bf16 forward output made of delta = dO . O.  The per-lane A' is one
+// running sum; D' and B are reduced over the 32 key lanes (transposed halving) and added into per-row LDS sums by
+// the wave that owns the row's block at that step (the staggered order: deterministic).
 constexpr int kSdRow = 32;   // bf16 per row of the [32 keys][32 queries] dS^T scratch (64 B)
 
 // element (k, q) of the dS^T scratch: 8-B column groups XOR-swizzled by k so that the packed stores (4 x 16 lanes,
 // bank (a/4) mod 32) and the tr16 reads (2 x 32 lanes, mod 64) are conflict-free
 __device__ __forceinline__ int sd_off(int k, int q) { return k * kSdRow + ((((q >> 2) ^ (k >> 1)) & 7) << 2) + (q & 3); }
 
-template <int HD, bool TAB, bool DROP>
+// halving reduction of 16 per-lane values over the 32 lanes of a half-wave: lane l ends with the sum of register
+// (l >> 1) & 15 over the 32 lanes (l = lane & 31)
+__device__ __forceinline__ float halving_sum16(float (&v)[16], int lane) {
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int n = 8 >> st, m = 16 >> st;
+    const bool lo = (lane & m) == 0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const float send = lo ? v[n + i] : v[i];
+      const float keep = lo ? v[i] : v[n + i];
+      v[i] = keep + __shfl_xor(send, m, 64);
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1, 64);
+}
+
+template <int HD, bool TAB, bool DROP, bool COS = false>
 __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_args ba, const Geo g, int q0, int Qn,
                                                          int accum_kv, bf16raw* __restrict__ dsg,
                                                          const bf16raw* __restrict__ tabb) {
@@ -2799,9 +2824,14 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   int* trow = reinterpret_cast<int*>(p); p += 4 * Np;
   float* nl2 = reinterpret_cast<float*>(p); p += 4 * Qn;   // -lse log2e; -inf beyond N (P = 0)
   float* ndl = reinterpret_cast<float*>(p); p += 4 * Qn;   // -delta
+  float* rowD = reinterpret_cast<float*>(p); p += COS ? 4 * Qn : 0;   // COS: D' and B per query row
+  float* rowB = reinterpret_cast<float*>(p); p += COS ? 4 * Qn : 0;
+  float* red = reinterpret_cast<float*>(p); p += COS ? 4 * 16 : 0;
+  static_assert(!(COS && (DROP || !TAB)), "COS: bias-table path without dropout");
 
   const int tid = dfk_tid(), lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  float accA = 0.f;
   const WUnit wu = decode_unit(a, g, 1);   // the forward's work order; lse / dS^T / dropout rows by lse_unit
   const int head = wu.head, win = wu.win, b = wu.b;
   const long unit = wu.lse_unit;
@@ -2819,6 +2849,8 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   for (int i = tid; i < Qn; i += dfk_bdim())
     nl2[i] = q0 + i < g.N ? -a.lse[unit * Np + q0 + i] * kLog2e : -INFINITY;
   for (int i = tid * 4; i < Qn * HD; i += dfk_bdim() * 4) *reinterpret_cast<f32x4*>(dQa + i) = f32x4{0, 0, 0, 0};
+  if constexpr (COS)
+    for (int i = tid; i < Qn; i += dfk_bdim()) rowD[i] = rowB[i] = 0.f;
   __syncthreads();
   // Q / dO / O gather, QB row chunks per thread in flight (all loads of a batch issued before the wait that
   // precedes their use: one HBM round trip per batch, not per chunk)
@@ -2937,6 +2969,12 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
         }
         load_bias(qb + 1 == nqb ? 0 : qb + 1);
       }
+      f32x16 cin;   // COS: the product alone is the score (rows beyond N: c = -inf, the product stays finite)
+      if constexpr (COS) {
+        cin = s;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) s[j] = 0.f;
+      }
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
         const int off = qr0 * HD + qoff[kk];
@@ -2944,6 +2982,11 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
         const bf16x8 da = *reinterpret_cast<const bf16x8*>(dOs + off);
         s = mfma32(qa, kB[kk], s);
         dp = mfma32(da, vB[kk], dp);
+      }
+      f32x16 raw;
+      if constexpr (COS) {
+        raw = s;
+        s = s + cin;
       }
 
       // P = 2^S', dS = P dP'; B-operand fragments of k-steps c (registers 8c .. 8c+7)
@@ -2963,6 +3006,20 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
             sa[c][j] = (__bf16)(P * dp[8 * c + j]);
           }
         }
+      float cosD = 0.f, cosB = 0.f;   // COS: this lane's row (register (r >> 1) & 15) sums over the block's keys
+      if constexpr (COS) {
+        float vd[16], vb[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float P = __builtin_amdgcn_exp2f(s[j]);
+          const float ds = P * dp[j];
+          accA += ds * raw[j];
+          vd[j] = ds;
+          vb[j] = P * raw[j];
+        }
+        cosD = halving_sum16(vd, lane);
+        cosB = halving_sum16(vb, lane);
+      }
       // dS^T -> the wave's scratch: registers 4v .. 4v+3 (queries 8v + 4hh + 0..3) at [key r][8v + 4hh]
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -3023,6 +3080,13 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
           f32x4* ap = reinterpret_cast<f32x4*>(dQa + ((size_t)((qb * NOT + ot) * 4 + v) * 64 + lane) * 4);
           *ap = *ap + f32x4{dq[ot][4 * v], dq[ot][4 * v + 1], dq[ot][4 * v + 2], dq[ot][4 * v + 3]};
         }
+      if constexpr (COS) {
+        if ((r & 1) == 0) {   // register j = (r >> 1) & 15 <-> query 8 (j >> 2) + 4 hh + (j & 3) of the block
+          const int j = (r >> 1) & 15, q = qr0 + 8 * (j >> 2) + 4 * hh + (j & 3);
+          rowD[q] += cosD;
+          rowB[q] += cosB;
+        }
+      }
     }
     // dK = scale sum dS q = (sum dS Q') ln 2, dV: lane holds key r, e = 32 ot + (j & 3) + 8 (j >> 2) + 4 hh
     const float kscale = 0.6931471805599453f;
@@ -3058,6 +3122,19 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
       }
   }
   __syncthreads();
+  if constexpr (COS) {   // dscore[head] += ln2 (sum A' - sum_q D'_q B_q): the score is r' ln 2 (r' in log2 units)
+    float t = accA;
+    for (int i = tid; i < Qn; i += dfk_bdim()) t -= rowD[i] * rowB[i];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) red[wave] = t;
+    __syncthreads();
+    if (tid == 0) {
+      float tot = 0.f;
+      for (int w = 0; w < nw; ++w) tot += red[w];
+      atomicAdd(ba.dscore + head, tot * 0.6931471805599453f);
+    }
+  }
   // dQ rows (scaled): (q, e) of block qb sits at [qb][ot][v][lane][t], q = 32 qb + 8 v + 4 h + t, lane = (e & 31) + 32 h
   for (int t8 = tid; t8 < Qn * (HD / 8); t8 += dfk_bdim()) {
     const int i = t8 / (HD / 8), c = (t8 % (HD / 8)) * 8;
@@ -3080,8 +3157,9 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   }
 }
 
-size_t bwd3_lds(const dfk_wattn_args& a, const Geo& g, int Qn, int nw) {
-  return 8 * (size_t)Qn * a.hd + 2 * (size_t)nw * 32 * kSdRow + 4 * (size_t)g.Np + 8 * (size_t)Qn;
+size_t bwd3_lds(const dfk_wattn_args& a, const Geo& g, int Qn, int nw, bool cos = false) {
+  return 8 * (size_t)Qn * a.hd + 2 * (size_t)nw * 32 * kSdRow + 4 * (size_t)g.Np + 8 * (size_t)Qn +
+         (cos ? 8 * (size_t)Qn + 64 : 0);
 }
 
 // dRPB from the dS^T scratch: drpb[pos(q) - pos(k) + C0] += sum over windows of dS[q][k].
@@ -3202,19 +3280,21 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     const bf16raw* tb = tab ? tab3_fwd(a, g) + tab_elems(a, g) : nullptr;
     const int nkb = g.Np / 32;
     int nw = dfk_cdiv(nkb, dfk_cdiv(nkb, 8));   // passes of at most 8 waves, balanced
+    const bool cos = bp->dscore != nullptr;
+    if (cos && (!tab || a.drop.mode)) return DFK_EINVAL;   // dscore: the bias-table path without dropout only
     int Qn = g.Np;                               // largest query chunk whose Q / dO / dQ fit the LDS ...
-    while (Qn > 32 && bwd3_lds(a, g, Qn, nw) > 160 * 1024) Qn -= 32;
+    while (Qn > 32 && bwd3_lds(a, g, Qn, nw, cos) > 160 * 1024) Qn -= 32;
     const int nch = dfk_cdiv(g.Np, Qn);          // ... then balanced chunks
     Qn = 32 * dfk_cdiv(g.Np / 32, nch);
     nw = std::min(nw, g.Np / 32 - (nch - 1) * (Qn / 32));   // the staggered sweep needs a distinct block per wave
-    const size_t lds = bwd3_lds(a, g, Qn, nw);
+    const size_t lds = bwd3_lds(a, g, Qn, nw, cos);
     if (lds > 160 * 1024) return DFK_EINVAL;
     const bool want_drpb = a.rpb && bp->drpb;
     if (want_drpb && !bp->ws) return DFK_EINVAL;
     bf16raw* dsg = want_drpb ? reinterpret_cast<bf16raw*>(bp->ws) : nullptr;
-#define LAUNCH_B3(HD, TB, DR)                                                                              \
+#define LAUNCH_B3(HD, TB, DR, CS)                                                                          \
   do {                                                                                                     \
-    auto kfn = wattn_bwd3_kernel<HD, TB, DR>;                                                              \
+    auto kfn = wattn_bwd3_kernel<HD, TB, DR, CS>;                                                            \
     static bool attr_set = false;                                                                          \
     if (!attr_set) {                                                                                       \
       (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
@@ -3226,8 +3306,9 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
   } while (0)
 #define PICK_B3(HD)                                                                            \
   do {                                                                                         \
-    if (tab) { if (a.drop.mode) LAUNCH_B3(HD, true, true); else LAUNCH_B3(HD, true, false); }  \
-    else { if (a.drop.mode) LAUNCH_B3(HD, false, true); else LAUNCH_B3(HD, false, false); }    \
+    if (cos) LAUNCH_B3(HD, true, false, true);                                                 \
+    else if (tab) { if (a.drop.mode) LAUNCH_B3(HD, true, true, false); else LAUNCH_B3(HD, true, false, false); } \
+    else { if (a.drop.mode) LAUNCH_B3(HD, false, true, false); else LAUNCH_B3(HD, false, false, false); }        \
   } while (0)
     if (a.hd == 32) PICK_B3(32); else PICK_B3(64);
 #undef PICK_B3
@@ -3244,6 +3325,7 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     DFK_CHECK_LAUNCH();
     return 0;
   }
+  if (bp->dscore) return DFK_EINVAL;   // the score-multiplier gradient: v3 (bias tables, bf16) only
   if (a.dtype == DFK_BF16) {
     const int nwaves = std::min(a.hd == 32 ? kBwdWaves : kBwdWaves / 2, g.Np / 32);  // hd 64: 4 waves, 512 VGPRs
     int Qn = g.Np;

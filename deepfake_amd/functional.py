@@ -5,6 +5,8 @@ read through ``compute_weight`` (the bf16 shadow kept by
 deepfake_amd.params.ParamStore, else a per-call cast) and every weight /
 bias gradient is produced in fp32.
 """
+import os
+
 import torch
 
 from . import kernels as K
@@ -364,7 +366,7 @@ class WindowAttnFn(torch.autograd.Function):
     [3C] (the padded positions' q/k/v, or None), explicit mask or None."""
 
     @staticmethod
-    def forward(ctx, qkv, rpb, qkv_bias, mask, geo, drop=None):
+    def forward(ctx, qkv, rpb, qkv_bias, mask, geo, drop=None, dscore=None):
         dims, window, full_window, shift, heads, hd, scale = geo
         C = heads * hd
         pads = None
@@ -381,7 +383,7 @@ class WindowAttnFn(torch.autograd.Function):
         grad_use(ctx, 1, rpb)
         grad_use(ctx, 2, qkv_bias)
         ctx.save_for_backward(qkv, out, lse, rpb_f, mask, rpb, qkv_bias)
-        ctx.pads, ctx.geo, ctx.drop = pads, geo, drop
+        ctx.pads, ctx.geo, ctx.drop, ctx.dscore = pads, geo, drop, dscore
         ctx.has_rpb, ctx.has_bias = rpb is not None, qkv_bias is not None
         return out
 
@@ -402,20 +404,39 @@ class WindowAttnFn(torch.autograd.Function):
         dpads = [dbias[i * C:(i + 1) * C] for i in range(3)] if ctx.has_bias else None
         K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, qkv.stride(0), dims, window, full_window, shift, heads,
                      hd, scale, rpb_f, ctx.pads), dout.contiguous(), dqkv, dqkv[:, C:], dqkv[:, 2 * C:], qkv.stride(0),
-                    drpb=drpb, dpads=dpads, mask=mask, tab=ctx.tab, drop=ctx.drop)
+                    drpb=drpb, dpads=dpads, mask=mask, tab=ctx.tab, drop=ctx.drop, dscore=ctx.dscore)
         ctx.tab = None
         if ctx.has_rpb:
             drpb = grad_done(rpb, drpb)
         if ctx.has_bias:
             dbias = grad_done(qkv_bias, dbias)
-        return dqkv, drpb, dbias, None, None, None
+        return dqkv, drpb, dbias, None, None, None, None
 
 
-def window_attention(qkv, rpb, qkv_bias, geo, mask=None, drop=None):
-    """drop: attention-probability dropout (bf16 table path only)."""
+def window_attention(qkv, rpb, qkv_bias, geo, mask=None, drop=None, dscore=None):
+    """drop: attention-probability dropout (bf16 table path only).  dscore: [heads] fp32 buffer the backward adds
+    sum dS * score into (SwinV2's logit_scale gradient, consumed and re-zeroed by CosineQKFn's backward; bf16
+    table path without dropout only — see dscore_buffer)."""
     if drop is not None and qkv.dtype != torch.bfloat16:
         raise NotImplementedError("attention dropout runs in the bf16 table kernels only (fp32 parity mode: p = 0)")
-    return WindowAttnFn.apply(qkv, rpb, qkv_bias, mask, geo, drop)
+    return WindowAttnFn.apply(qkv, rpb, qkv_bias, mask, geo, drop, dscore)
+
+
+def dscore_buffer(owner, qkv, heads, drop):
+    """The [heads] fp32 buffer through which the attention backward hands sum dS * score to CosineQKFn's backward
+    (dfk_wattn_bwd_args.dscore), or None where the attention kernel cannot produce it (fp32 parity mode, attention
+    dropout, the table path switched off): CosineQKFn then derives the logit_scale gradient from q-hat . dq'.
+    Persistent per module (zeroed once; the consumer re-zeroes it), so a captured step holds no fill for it."""
+    if qkv.dtype != torch.bfloat16 or drop is not None or os.environ.get("DFK_WATTN_TABLE", "1") == "0" \
+            or os.environ.get("DFK_COS_DSCORE", "1") == "0":
+        return None
+    buf = getattr(owner, "_dfk_dscore", None)
+    if buf is None or buf.device != qkv.device or buf.numel() != heads:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("dscore buffer created inside a graph capture (run one eager step first)")
+        buf = torch.zeros(heads, device=qkv.device, dtype=torch.float32)
+        owner._dfk_dscore = buf
+    return buf
 
 
 class DropoutFn(torch.autograd.Function):
@@ -612,7 +633,7 @@ class CosineQKFn(torch.autograd.Function):
     (swin_transformer2d.py:154-157); the logit_scale gradient is accumulated directly."""
 
     @staticmethod
-    def forward(ctx, qkv, logit_scale, heads, hd, max_log):
+    def forward(ctx, qkv, logit_scale, heads, hd, max_log, dscore=None):
         out = torch.empty_like(qkv)
         ls = logit_scale.detach()
         if ls.dtype != torch.float32 or not ls.is_contiguous():
@@ -621,7 +642,7 @@ class CosineQKFn(torch.autograd.Function):
                                               heads, hd, K.L.dt(qkv), K.L.stream()), "cosine_qk_fwd")
         grad_use(ctx, 1, logit_scale)
         ctx.save_for_backward(qkv, ls, logit_scale)
-        ctx.hd, ctx.max_log = hd, max_log
+        ctx.hd, ctx.max_log, ctx.dscore = hd, max_log, dscore
         return out
 
     @staticmethod
@@ -632,8 +653,9 @@ class CosineQKFn(torch.autograd.Function):
         dls = grad_sink(logit_scale) if logit_scale.dtype == torch.float32 else torch.zeros_like(ls)
         K.L.check(K.L.lib().dfk_cosine_qk_bwd(K.L.ptr(qkv), K.L.ptr(dout.contiguous()), K.L.ptr(dqkv), K.L.ptr(ls),
                                               float(ctx.max_log), K.L.ptr(dls), qkv.shape[0], heads, ctx.hd,
-                                              K.L.dt(qkv), K.L.stream()), "cosine_qk_bwd")
-        return dqkv, grad_done(logit_scale, dls.view_as(logit_scale)), None, None, None
+                                              K.L.dt(qkv), K.L.ptr(ctx.dscore) if ctx.dscore is not None else None,
+                                              K.L.stream()), "cosine_qk_bwd")
+        return dqkv, grad_done(logit_scale, dls.view_as(logit_scale)), None, None, None, None
 
 
 class CPBBiasFn(torch.autograd.Function):
@@ -665,18 +687,23 @@ class CPBBiasFn(torch.autograd.Function):
 
 
 _CPB_DESC = {}   # (pointers, dims) -> device descriptor array of dfk_cpb_bias_*_many (built once, replay-safe)
+_CPB_PINNED = set()   # keys a graph capture read: a captured graph dereferences them at every replay
 
 
-def _cpb_desc(rows):
-    key = tuple(tuple(r) for r in rows)
+def _cpb_desc(rows, device):
+    key = tuple(tuple(r) for r in rows) + (str(device),)
     d = _CPB_DESC.get(key)
+    capturing = torch.cuda.is_current_stream_capturing()
     if d is None:
-        if torch.cuda.is_current_stream_capturing():
+        if capturing:
             raise RuntimeError("cpb descriptor built inside a graph capture (run one eager step first)")
-        d = torch.tensor([v for r in rows for v in r], dtype=torch.int64).cuda()
+        d = torch.tensor([v for r in rows for v in r], dtype=torch.int64, device=device)
         if len(_CPB_DESC) > 64:   # modules without a ParamStore get fresh gradient buffers every call
-            _CPB_DESC.clear()
+            for k in [k for k in _CPB_DESC if k not in _CPB_PINNED]:
+                del _CPB_DESC[k]
         _CPB_DESC[key] = d
+    if capturing:
+        _CPB_PINNED.add(key)
     return d
 
 
@@ -702,7 +729,7 @@ class CPBManyFn(torch.autograd.Function):
             off += L * heads
         out = torch.empty(off, device=cs[0].device, dtype=torch.float32)
         maxL = max(d[1] for d in dims)
-        K.L.check(K.L.lib().dfk_cpb_bias_fwd_many(K.L.ptr(_cpb_desc(fwd_rows)), n, maxL, K.L.ptr(out),
+        K.L.check(K.L.lib().dfk_cpb_bias_fwd_many(K.L.ptr(_cpb_desc(fwd_rows, out.device)), n, maxL, K.L.ptr(out),
                                                    K.L.stream()), "cpb_bias_fwd_many")
         for i, p in enumerate(params):
             grad_use(ctx, 1 + n + i, p)
@@ -732,7 +759,7 @@ class CPBManyFn(torch.autograd.Function):
         ctx.gbuf = None
         sinks = [grad_sink(p) for p in params]
         rows = [r[:4] + [t.data_ptr() for t in sinks[3 * i:3 * i + 3]] + r[7:] for i, r in enumerate(ctx.fwd_rows)]
-        K.L.check(K.L.lib().dfk_cpb_bias_bwd_many(K.L.ptr(_cpb_desc(rows)), n, ctx.maxL, K.L.ptr(out),
+        K.L.check(K.L.lib().dfk_cpb_bias_bwd_many(K.L.ptr(_cpb_desc(rows, out.device)), n, ctx.maxL, K.L.ptr(out),
                                                    K.L.ptr(dflat), K.L.stream()), "cpb_bias_bwd_many")
         return (None,) + (None,) * n + tuple(grad_done(p, g) for p, g in zip(params, sinks))
 

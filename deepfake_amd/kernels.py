@@ -178,8 +178,8 @@ def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None, residual=No
 _DW_MIN_K = int(os.environ.get("DFK_DW_MINK", "512"))   # tokens per split of a weight-gradient GEMM (tuning)
 _DW_UNSPLIT64 = int(os.environ.get("DFK_DW_UNSPLIT64", "384"))   # 64x64 tiles from which dW runs unsplit (r5o: the
 # 256-tile SwinV2 stage-3 fc1 / fc2 dW 22 -> 19, 21 -> 19 us on split 128x128 tiles; w2v (432-576 tiles) flat)
-_DW_XCD = int(os.environ.get("DFK_DW_XCD", "1"))
-_DW_SLAB = os.environ.get("DFK_DW_SLAB", "0") == "1"   # split counts rounded to multiples of 8 (XCD grouping; A/B knob)
+_DW_XCD = int(os.environ.get("DFK_DW_XCD", "1"))   # split counts rounded to multiples of 8 (XCD grouping; A/B knob)
+_DW_SLAB = os.environ.get("DFK_DW_SLAB", "0") == "1"   # fp32 split slabs + one reduce instead of split atomics (A/B knob)
 
 
 def splitk_for(tiles, K, min_k=None):
@@ -331,7 +331,8 @@ def wattn_fwd_policy(version=-1, bal_min_units=-1):
     L.check(L.lib().dfk_wattn_fwd_policy(int(version), int(bal_min_units)), "wattn_fwd_policy")
 
 
-def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None, mask=None, tab=None, drop=None):
+def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None, mask=None, tab=None, drop=None,
+              dscore=None):
     """Backward of wattn_fwd.  fwd_args_tensors = (q, k, v, out, lse, ld_qkv, dims, window, full_window,
     shift, heads, hd, scale, rpb, pads).  dq/dk/dv may alias column slices of one [rows, 3C] buffer."""
     (q, k, v, out, lse, ld_qkv, dims, window, full_window, shift, heads, hd, scale, rpb, pads) = fwd_args_tensors
@@ -347,6 +348,7 @@ def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None
         ba.dpad_q, ba.dpad_k, ba.dpad_v = (p.data_ptr() for p in dpads)
     ba.ld_dqkv = int(ld_dqkv)
     ba.ld_dout = int(dout.stride(0))
+    ba.dscore = dscore.data_ptr() if dscore is not None else None
     ws = None
     if drpb is not None:
         nbytes = L.lib().dfk_wattn_bwd_workspace(ba.f)

@@ -117,12 +117,15 @@ class WindowAttention(nn.Module):
                 qkv, xs = qkv
         else:
             qkv = Fn.linear(x2d, self.qkv.weight)
-        qkv = Fn.CosineQKFn.apply(qkv, self.logit_scale, self.num_heads, hd, math.log(1. / 0.01))
+        ad = self.attn_drop.spec() if self.attn_drop is not None and self.training else None
+        # logit_scale's gradient: sum dS * score taken in fp32 inside the attention backward (dfk_wattn_bwd_args
+        # .dscore), handed to the cosine backward through a per-module buffer
+        dsc = Fn.dscore_buffer(self, qkv, self.num_heads, ad) if self.logit_scale.requires_grad else None
+        qkv = Fn.CosineQKFn.apply(qkv, self.logit_scale, self.num_heads, hd, math.log(1. / 0.01), dsc)
         geo = (dims, (1, ws, ws), (1, self.window_size[0], self.window_size[1]), (0, shift, shift),
                self.num_heads, hd, 1.0)
-        ad = self.attn_drop.spec() if self.attn_drop is not None and self.training else None
         tab = self._cpb if getattr(self, "_cpb", None) is not None else self.bias_table()
-        out = Fn.window_attention(qkv, tab, None, geo, drop=ad)
+        out = Fn.window_attention(qkv, tab, None, geo, drop=ad, dscore=dsc)
         return (out, xs) if skip else out
 
 

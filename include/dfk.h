@@ -230,6 +230,11 @@ typedef struct {
   float* dpad_q; float* dpad_k; float* dpad_v;
   int64_t ld_dqkv, ld_dout;
   float* ws;
+  float* dscore;        /* NULL, or [heads] fp32 (+=): sum over rows and keys of dS * score (the score before
+                           the bias, scale q.k) = the gradient of a per-head multiplier of the scores — SwinV2's
+                           logit_scale (swin_transformer2d.py:155-157: attn = cos(q,k) * exp(logit_scale)), taken in
+                           fp32 inside the backward with the exact softmax-backward row constant.  bf16 bias-table
+                           path without dropout only (else DFK_EINVAL) */
 } dfk_wattn_bwd_args;
 int dfk_wattn_bwd(const dfk_wattn_bwd_args* a, hipStream_t stream);
 int64_t dfk_wattn_bwd_workspace(const dfk_wattn_args* f);
@@ -312,8 +317,12 @@ int dfk_w2v_conv0_bwd(const float* wave, int64_t B, int64_t S, const float* w, c
  * The backward writes dqkv and accumulates the logit_scale gradient dlogit_scale[h] (fp32 +=). */
 int dfk_cosine_qk_fwd(const void* qkv, void* out, const float* logit_scale, float max_log, int64_t rows, int heads,
                       int hd, int dtype, hipStream_t stream);
+/* dscore: NULL (the logit_scale gradient from q-hat . dq' here), or the [heads] fp32 sum of dS * score that
+ * dfk_wattn_bwd accumulated (dfk_wattn_bwd_args.dscore): then dlogit_scale[h] += dscore[h] where logit_scale[h]
+ * <= max_log, and dscore is set back to zero for the next step. */
 int dfk_cosine_qk_bwd(const void* qkv, const void* dout, void* dqkv, const float* logit_scale, float max_log,
-                      float* dlogit_scale, int64_t rows, int heads, int hd, int dtype, hipStream_t stream);
+                      float* dlogit_scale, int64_t rows, int heads, int hd, int dtype, float* dscore,
+                      hipStream_t stream);
 
 /* SwinV2 continuous position bias (swin_transformer2d.py:99-100,159-162): out[l][h] =
  * 16 * sigmoid(sum_j W2[h][j] * relu(W1[j][0]*c[l][0] + W1[j][1]*c[l][1] + b1[j])) for the L = (2Wh-1)(2Ww-1)

@@ -120,12 +120,14 @@ def test_linear_dw_token_streaming(M, N, Kd, monkeypatch):
 
 
 @pytest.mark.parametrize("slab", [False, True])
-@pytest.mark.parametrize("M,N,Kd", [(50176, 96, 96), (40000, 384, 96), (1568, 2048, 512), (1592, 768, 3072)])
+@pytest.mark.parametrize("M,N,Kd", [(50176, 96, 96), (40000, 384, 96), (1568, 2048, 512), (1592, 768, 3072),
+                                    (40000, 100, 96), (40000, 96, 100)])
 def test_linear_dw_bias_partials(M, N, Kd, slab, monkeypatch):
     """The weight gradient with its fused bias gradient on every split path: >= 32 atomic splits (the stage-1
     shapes: per-split bias partials + rowsum_reduce_kernel), few atomic splits (bias atomics), unsplit, and the fp32
     split-slab path (kernels._DW_SLAB: slab_sum_f32_kernel, bias partials after the slab) — against fp64, into
-    non-zero dW / db."""
+    non-zero dW / db.  N or Kd not a multiple of 8 runs the register-staged kernel, which adds the bias gradient
+    atomically and writes no partials: no partial reduce may run on that path."""
     monkeypatch.setattr(K, "_DW_SLAB", slab)
     g = torch.Generator(device=DEV).manual_seed(7)
     x = torch.randn(M, Kd, device=DEV, generator=g).to(torch.bfloat16)
@@ -329,3 +331,64 @@ def test_rowmean(dt, groups, R, C):
     out = K.rowmean(x, groups)
     ref = x.float().view(groups, R, C).mean(1)
     assert rel(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("heads,clamped,H", [(4, False, 14), (8, True, 21)])
+def test_cosine_attention_logit_scale_dscore(heads, clamped, H):
+    """SwinV2 window attention (swin_transformer2d.py:140-179: cosine scores * exp(clamp(logit_scale)) + 16
+    sigmoid CPB bias, softmax, @ v) in bf16: the logit_scale gradient taken inside the attention backward
+    (dfk_wattn_bwd_args.dscore: sum dS * score in fp32 with the exact softmax-backward row constant) against fp64
+    autograd on the same bf16 inputs, and against the q-hat . dq' fallback (dscore off), which it must not lose to.
+    The sum cancels to a few % of its terms, so its error is the precision of the whole chain."""
+    from deepfake_amd import functional as Fn
+    g = torch.Generator(device=DEV).manual_seed(21 + heads)
+    B, W, ws, hd = 2, H, 7, 32
+    C = heads * hd
+    rows = B * H * W
+    qkv = torch.randn(rows, 3 * C, device=DEV, generator=g).to(torch.bfloat16)
+    L = (2 * ws - 1) ** 2
+    tab = (16 * torch.sigmoid(torch.randn(L, heads, device=DEV, generator=g))).contiguous()
+    logit0 = torch.rand(heads, 1, 1, device=DEV, generator=g) * 2 + (4.0 if clamped else 1.5)
+    dout = torch.randn(rows, C, device=DEV, generator=g).to(torch.bfloat16)
+    geo = ((B, 1, H, W), (1, ws, ws), (1, ws, ws), (0, 0, 0), heads, hd, 1.0)
+    max_log = math.log(100.0)
+
+    def run(use_dscore):
+        logit = logit0.clone().requires_grad_(True)
+        x = qkv.clone().requires_grad_(True)
+        dsc = torch.zeros(heads, device=DEV) if use_dscore else None
+        y = Fn.CosineQKFn.apply(x, logit, heads, hd, max_log, dsc)
+        out = Fn.window_attention(y, tab, None, geo, dscore=dsc)
+        out.backward(dout)
+        if dsc is not None:
+            assert dsc.abs().max().item() == 0.0   # consumed and re-zeroed by the cosine backward
+        return out.detach(), logit.grad.flatten(), x.grad
+
+    # fp64 reference on the same bf16 inputs
+    lr = logit0.double().clone().requires_grad_(True)
+    xr = qkv.double().clone().requires_grad_(True)
+    q, k, v = (xr[:, i * C:(i + 1) * C].view(B, H // ws, ws, W // ws, ws, heads, hd) for i in range(3))
+    part = lambda t: t.permute(0, 1, 3, 5, 2, 4, 6).reshape(-1, heads, ws * ws, hd)
+    q, k, v = part(q), part(k), part(v)
+    s = torch.clamp(lr, max=max_log).exp()
+    attn = torch.nn.functional.normalize(q, dim=-1) @ torch.nn.functional.normalize(k, dim=-1).transpose(-1, -2)
+    attn = attn * s
+    yy, xx = torch.meshgrid(torch.arange(ws), torch.arange(ws), indexing="ij")
+    pos = (yy * (2 * ws - 1) + xx).flatten().to(DEV)
+    idx = pos[:, None] - pos[None, :] + (ws - 1) * (2 * ws - 1) + (ws - 1)
+    attn = attn + tab.double()[idx].permute(2, 0, 1).unsqueeze(0)
+    o = torch.softmax(attn, -1) @ v
+    o = o.view(B, H // ws, W // ws, heads, ws, ws, hd).permute(0, 1, 4, 2, 5, 3, 6).reshape(rows, C)
+    o.backward(dout.double())
+    ref = lr.grad.flatten()
+
+    out_n, dl_n, dx_n = run(True)
+    out_o, dl_o, dx_o = run(False)
+    assert torch.equal(out_n, out_o)
+    assert torch.equal(dx_n, dx_o)   # the q / k / v gradients do not depend on where dlogit is taken
+    assert rel(out_n, o) < 2e-2
+    err_n = ((dl_n.double() - ref).abs() / ref.abs().clamp_min(1e-30)).max().item()
+    err_o = ((dl_o.double() - ref).abs() / ref.abs().clamp_min(1e-30)).max().item()
+    print(f"logit_scale grad rel err: dscore {err_n:.3e}, q-hat.dq' {err_o:.3e}")
+    assert err_n < 1e-2
+    assert err_n <= err_o * 1.5 + 1e-4
