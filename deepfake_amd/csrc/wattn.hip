@@ -650,6 +650,61 @@ __device__ __forceinline__ WUnit decode_unit(const dfk_wattn_args& a, const Geo&
   return w;
 }
 
+// Backward work groups (dRPB): one workgroup runs G windows of one (shift class, head) in turn and adds their dS^T
+// into ONE slab of the dRPB scratch (the first window stores, the later ones read-modify-write the same tiles, which
+// the same lanes wrote: a fixed order, no atomics), so the scratch and its reduction shrink G-fold.  Classes in the
+// forward's order; inside a class, head innermost (consecutive workgroups gather the same qkv rows).
+struct WGroup {
+  int cls, head, t, n;   // class, head, group index in the class, windows in this group
+  int nd, nh, nw;        // the class's window counts
+  long slab;             // scratch slab: (groups of the earlier classes + t) * heads + head
+};
+
+__device__ __forceinline__ WGroup decode_group(const dfk_wattn_args& a, const Geo& g, int G) {
+  const int total = dfk_gdim_x(), bid = dfk_bid_x();
+  const int xcd = bid & 7, per = total >> 3, rr = total & 7;
+  int u = (xcd < rr ? xcd * (per + 1) : rr * (per + 1) + (xcd - rr) * per) + (bid >> 3);
+  const int ncls = g.use_mask ? 8 : 1;
+  int c = 0, nd = g.nwd, nh = g.nwh, nw = g.nww;
+  long gacc = 0;
+  int cntw = 0;
+  for (; c < ncls; ++c) {
+    nd = g.use_mask ? ((c & 4) ? (a.sd > 0) : g.nwd - (a.sd > 0)) : g.nwd;
+    nh = g.use_mask ? ((c & 2) ? (a.sh > 0) : g.nwh - (a.sh > 0)) : g.nwh;
+    nw = g.use_mask ? ((c & 1) ? (a.sw > 0) : g.nww - (a.sw > 0)) : g.nww;
+    cntw = nd * nh * nw * a.B;
+    const int ngr = (cntw + G - 1) / G;
+    if (u < ngr * a.heads) break;
+    u -= ngr * a.heads;
+    gacc += ngr;
+  }
+  WGroup r;
+  r.cls = c;
+  r.head = u % a.heads;
+  r.t = u / a.heads;
+  r.n = min(G, cntw - r.t * G);
+  r.nd = nd; r.nh = nh; r.nw = nw;
+  r.slab = (gacc + r.t) * a.heads + r.head;
+  return r;
+}
+
+__device__ __forceinline__ WUnit group_window(const dfk_wattn_args& a, const Geo& g, const WGroup& gr, int G, int gi) {
+  const int perw = gr.nd * gr.nh * gr.nw;
+  int wl = gr.t * G + gi;
+  WUnit w;
+  w.qpart = 0;
+  w.head = gr.head;
+  w.cls = gr.cls;
+  w.b = wl / perw;
+  wl %= perw;
+  const int id = wl / (gr.nh * gr.nw), ih = (wl / gr.nw) % gr.nh, iw = wl % gr.nw;
+  const int c = gr.cls;
+  const int wdi = (c & 4) ? g.nwd - 1 : id, whi = (c & 2) ? g.nwh - 1 : ih, wwi = (c & 1) ? g.nww - 1 : iw;
+  w.win = (wdi * g.nwh + whi) * g.nww + wwi;
+  w.lse_unit = ((long)w.b * g.nW + w.win) * a.heads + w.head;
+  return w;
+}
+
 // wattn.hip is compiled with IEEE mode off and no-NaN semantics (build.py FILE_FLAGS), so fmaxf chains
 // become v_max3_f32 without operand canonicalisation.
 __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
@@ -1613,7 +1668,10 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // (k-slots j <-> key 16 (j >> 2) + 4 (l >> 4) + (j & 3)), and V^T is read with the same slot order by ds_read_tr16.
 // Row statistics are per (chain, half) and reduce over the 4 lane groups.  Bias tables in the fwd16 layout
 // (wattn_tab3_kernel fwd16: [qh][64 lanes][kh][r]).
-template <bool BAL>
+// ONES (A/B, non-BAL only): the softmax denominators by a third PV-shaped MFMA with an all-ones A operand (every
+// output row = the column's sum of the bf16 P that also multiplies V) instead of 8 VALU adds per query half and
+// the lane-group sum at the store: -16 VALU adds per 32x32 block for +2 MFMAs on the matrix pipe, which has slack
+template <bool BAL, bool ONES = false>
 __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args a, const Geo g, int qsplit,
                                                            const bf16raw* __restrict__ tab) {
   constexpr int HD = 32, CH = HD / 8;
@@ -1696,6 +1754,16 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
     };
     uint4 bt[2][2];
     load_bias(bt, k0);
+    f32x4 lac[2][2];   // ONES: the denominators as MFMA accumulators (all four registers hold the column's sum)
+    bf16x8 ones;
+    if constexpr (ONES) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) lac[u][qh] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     for (int kb = k0; kb < k1; ++kb) {
       const bf16raw* kbase = Ks + kb * 32 * HD;
       const bf16raw* vbase = Vs + kb * 32 * HD;
@@ -1748,6 +1816,7 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
                 d1[j] -= delta;
               }
               ls[u][qh] *= alpha;
+              if constexpr (ONES) lac[u][qh] = lac[u][qh] * alpha;
 #pragma unroll
               for (int j = 0; j < 8; ++j) o[u][8 * qh + j] *= alpha;
             }
@@ -1758,10 +1827,11 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
             p[j] = __builtin_amdgcn_exp2f(d0[j]);
             p[4 + j] = __builtin_amdgcn_exp2f(d1[j]);
           }
-          ls[u][qh] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+          if constexpr (!ONES) ls[u][qh] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
           bf16x8 pv;
 #pragma unroll
           for (int j = 0; j < 8; ++j) pv[j] = (__bf16)p[j];
+          if constexpr (ONES) lac[u][qh] = mfma16(ones, pv, lac[u][qh]);
 #pragma unroll
           for (int eh = 0; eh < 2; ++eh) {
             f32x4 acc = {o[u][8 * qh + 4 * eh], o[u][8 * qh + 4 * eh + 1], o[u][8 * qh + 4 * eh + 2],
@@ -1772,6 +1842,12 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
           }
         }
       }
+    }
+    if constexpr (ONES) {
+#pragma unroll
+      for (int u = 0; u < NC; ++u)
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) ls[u][qh] += lac[u][qh][0];
     }
   };
   auto zero = [&](f32x16 (&o)[2], float (&ls)[2][2], float (&m)[2][2]) __attribute__((always_inline)) {
@@ -1821,7 +1897,7 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
     float ls[2][2], m[2][2];
     zero(o, ls, m);
     chains(I1{}, SAFE{}, qbs, qf, 0, nkb, o, ls, m);
-    store(qb, o[0], ls[0], m[0]);
+    store(qb, o[0], ls[0], m[0], true, ONES);
   };
   auto full = [&](int qb0, int qb1) __attribute__((always_inline)) {
     const int qb[2] = {qb0, min(qb1, nqb - 1)};
@@ -1832,14 +1908,15 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
     float ls[2][2], m[2][2];
     zero(o, ls, m);
     chains(I2{}, FAST{}, qb, qf, 0, nkb, o, ls, m);
-    bool bad = store(qb[0], o[0], ls[0], m[0]);
-    bad |= store(qb[1], o[1], ls[1], m[1], qb1 < nqb);
+    bool bad = store(qb[0], o[0], ls[0], m[0], true, ONES);
+    bad |= store(qb[1], o[1], ls[1], m[1], qb1 < nqb, ONES);
     if (__builtin_amdgcn_ballot_w64(bad) != 0) {
       safe_block(qb[0]);
       if (qb1 < nqb) safe_block(qb1);
     }
   };
   const int nw = dfk_bdim() >> 6;
+  static_assert(!(BAL && ONES), "ONES: the simple schedule only");
   if constexpr (!BAL) {
     const int ngrp = (nqb + 1) / 2, qstep = nw * qsplit;
     for (int gi = wu.qpart * nw + wave; gi < ngrp; gi += qstep) full(2 * gi, 2 * gi + 1);
@@ -2007,6 +2084,7 @@ static long g_fwd_bal_min = getenv("DFK_WATTN_BALMIN") ? atol(getenv("DFK_WATTN_
 // 1.1 % in the reference's own bf16 run — the same attention error, rms 2.8e-3 either way, tools/wattn_err.py, in a
 // gradient that cancels to a few % of its terms)
 static const int g_v6_min_qb = getenv("DFK_WATTN_V6MIN") ? atoi(getenv("DFK_WATTN_V6MIN")) : 4;   // A/B runs only
+static const int g_v6_ones = getenv("DFK_WATTN_ONES") ? atoi(getenv("DFK_WATTN_ONES")) : 0;      // A/B runs only
 static bool use_v6(const dfk_wattn_args& a, const Geo& g) {
   return g_fwd_version == 6 && a.hd == 32 && !a.drop.mode && g.Np / 32 >= g_v6_min_qb;
 }
@@ -2096,6 +2174,7 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
       if (tab) {
         if (a.drop.mode) LAUNCH_K((wattn_fwd4_kernel<32, true, 1>));
         else if (v6 && bal) LAUNCH_K((wattn_fwd6_kernel<true>));
+        else if (v6 && g_v6_ones) LAUNCH_K((wattn_fwd6_kernel<false, true>));
         else if (v6) LAUNCH_K((wattn_fwd6_kernel<false>));
         else if (bal) LAUNCH_K((wattn_fwd5_kernel<true>));
         else if (v5) LAUNCH_K((wattn_fwd5_kernel<false>));
@@ -2788,6 +2867,16 @@ constexpr int kSdRow = 32;   // bf16 per row of the [32 keys][32 queries] dS^T s
 // bank (a/4) mod 32) and the tr16 reads (2 x 32 lanes, mod 64) are conflict-free
 __device__ __forceinline__ int sd_off(int k, int q) { return k * kSdRow + ((((q >> 2) ^ (k >> 1)) & 7) << 2) + (q & 3); }
 
+// two packed bf16 pairs + two packed bf16 pairs, fp32 add, round to nearest even
+__device__ __forceinline__ uint2 add_bf16x4(uint2 x, uint2 y) {
+  auto add2 = [](uint32_t p, uint32_t q) {
+    const float lo = __uint_as_float(p << 16) + __uint_as_float(q << 16);
+    const float hi = __uint_as_float(p & 0xffff0000u) + __uint_as_float(q & 0xffff0000u);
+    return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  };
+  return make_uint2(add2(x.x, y.x), add2(x.y, y.y));
+}
+
 // halving reduction of 16 per-lane values over the 32 lanes of a half-wave: lane l ends with the sum of register
 // (l >> 1) & 15 over the 32 lanes (l = lane & 31)
 __device__ __forceinline__ float halving_sum16(float (&v)[16], int lane) {
@@ -2808,7 +2897,7 @@ __device__ __forceinline__ float halving_sum16(float (&v)[16], int lane) {
 template <int HD, bool TAB, bool DROP, bool COS = false>
 __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_args ba, const Geo g, int q0, int Qn,
                                                          int accum_kv, bf16raw* __restrict__ dsg,
-                                                         const bf16raw* __restrict__ tabb) {
+                                                         const bf16raw* __restrict__ tabb, int G) {
   constexpr int NKK = HD / 16, NOT = HD / 32, CH = HD / 8;
   const dfk_wattn_args& a = ba.f;
   const int nw = dfk_bdim() >> 6;
@@ -2831,8 +2920,11 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
 
   const int tid = dfk_tid(), lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  const WGroup gr = decode_group(a, g, G);   // G windows of one (class, head), one dRPB scratch slab
+  for (int gi = 0; gi < gr.n; ++gi) {
   float accA = 0.f;
-  const WUnit wu = decode_unit(a, g, 1);   // the forward's work order; lse / dS^T / dropout rows by lse_unit
+  const WUnit wu = group_window(a, g, gr, G, gi);   // lse / dropout rows by lse_unit
+  const bool rmw = gi > 0;                          // later windows add into the slab the first one stored
   const int head = wu.head, win = wu.win, b = wu.b;
   const long unit = wu.lse_unit;
   const int hoff = head * HD;
@@ -2890,7 +2982,7 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
 
   bf16raw* Sw = Sd + wave * 32 * kSdRow;
   const DropCtx dc = drop_ctx(a.drop);
-  bf16raw* dsu = dsg ? dsg + unit * Np * Np : nullptr;   // this window-head's dS^T [k][q]
+  bf16raw* dsu = dsg ? dsg + gr.slab * Np * Np : nullptr;   // the group's dS^T slab [k][q]
   // per-lane LDS offsets (the tile swizzle sees a row only through bits a 32-row block step and a 16-row
   // k-step leave unchanged): Q' / dO row fragments (+ qr0 HD) and the transposed tr16 reads (+ qr0 HD + 16 c HD)
   int qoff[NKK], tlo[NOT], thi[NOT];
@@ -2944,6 +3036,13 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
     load_bias(qb);
     for (int i = 0; i < nqb; ++i, qb = qb + 1 == nqb ? 0 : qb + 1) {
       const int qr0 = qb * 32;   // local row of the block in the chunk
+      // the slab's earlier sum of this tile (later windows of the group): loaded now, added at the store
+      bf16raw* const gp = dsu ? dsu + (long)(kb * 32 + (lane >> 1)) * Np + q0 + qr0 + (lane & 1) * 16 : nullptr;
+      uint4 old0 = make_uint4(0, 0, 0, 0), old1 = old0;
+      if (dsu && rmw) {
+        old0 = *reinterpret_cast<const uint4*>(gp);
+        old1 = *reinterpret_cast<const uint4*>(gp + 8);
+      }
       // row constants as the C inputs: queries q0 + 8 v + 4 hh + (0..3) in registers 4v .. 4v+3
       f32x16 s, dp;
 #pragma unroll
@@ -3056,11 +3155,16 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
       }
       if (dsu) {   // scratch rows (32 keys x 64 B) -> global dS^T[k][q]: lane (key kr, half) un-swizzles 2 x 16 B
         const int kr = lane >> 1, half = lane & 1;
-        const uint2 x0 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16));
-        const uint2 x1 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 4));
-        const uint2 x2 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 8));
-        const uint2 x3 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 12));
-        bf16raw* gp = dsu + (long)(kb * 32 + kr) * Np + q0 + qr0 + half * 16;
+        uint2 x0 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16));
+        uint2 x1 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 4));
+        uint2 x2 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 8));
+        uint2 x3 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 12));
+        if (rmw) {
+          x0 = add_bf16x4(x0, make_uint2(old0.x, old0.y));
+          x1 = add_bf16x4(x1, make_uint2(old0.z, old0.w));
+          x2 = add_bf16x4(x2, make_uint2(old1.x, old1.y));
+          x3 = add_bf16x4(x3, make_uint2(old1.z, old1.w));
+        }
 #ifdef DFK_DS_NT
         typedef unsigned int u32x4n __attribute__((ext_vector_type(4)));
         __builtin_nontemporal_store(u32x4n{x0.x, x0.y, x1.x, x1.y}, reinterpret_cast<u32x4n*>(gp));
@@ -3155,6 +3259,8 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
       for (int j = 0; j < 8; ++j) atomicAdd(ba.dpad_q + hoff + c + j, vv[j]);
     }
   }
+  __syncthreads();   // the next window of the group reuses trow / dQa / the statistics
+  }
 }
 
 size_t bwd3_lds(const dfk_wattn_args& a, const Geo& g, int Qn, int nw, bool cos = false) {
@@ -3230,12 +3336,33 @@ struct DsPlan {
   long rows;       // workspace rows of L floats
 };
 
-DsPlan ds_plan(const dfk_wattn_args& a, const Geo& g) {
-  DsPlan pl;
+// windows per backward work group (wattn_bwd3_kernel, decode_group): enough groups left for ~3 rounds of one
+// workgroup per CU (768), at most 8 (DFK_DRPB_G: A/B runs only)
+int g_bwd_group = getenv("DFK_DRPB_G") ? atoi(getenv("DFK_DRPB_G")) : 0;   // dfk_wattn_bwd_policy
+int bwd3_group(const dfk_wattn_args& a, const Geo& g) {
+  if (g_bwd_group > 0) return g_bwd_group;
   const long units = (long)a.B * g.nW * a.heads;
+  return (int)std::max<long>(1, std::min<long>(8, units / 768));
+}
+
+// dS^T slabs per head (window groups over the shift classes, as decode_group counts them)
+long bwd3_slab_windows(const dfk_wattn_args& a, const Geo& g, int G) {
+  const int ncls = g.use_mask ? 8 : 1;
+  long tot = 0;
+  for (int c = 0; c < ncls; ++c) {
+    const long nd = g.use_mask ? ((c & 4) ? (a.sd > 0) : g.nwd - (a.sd > 0)) : g.nwd;
+    const long nh = g.use_mask ? ((c & 2) ? (a.sh > 0) : g.nwh - (a.sh > 0)) : g.nwh;
+    const long nw = g.use_mask ? ((c & 1) ? (a.sw > 0) : g.nww - (a.sw > 0)) : g.nww;
+    tot += dfk_cdiv(nd * nh * nw * a.B, (long)G);
+  }
+  return tot;
+}
+
+DsPlan ds_plan(const dfk_wattn_args& a, const Geo& g, long nwin) {
+  DsPlan pl;
+  const long units = nwin * a.heads;   // slabs (a window group's summed dS^T, or one window's)
   pl.ds_elems = units * g.Np * g.Np;
   pl.nchunks = (int)dfk_cdiv((long)g.Np * g.Np, 256 * 8);
-  const long nwin = units / a.heads;
   // about 1.5k workgroups over the chip, each summing wps windows (fewer, longer sums: fewer partial rows)
   const long want = std::max<long>(1, std::min<long>(nwin, 1536 / std::max(1, pl.nchunks * a.heads)));
   pl.wps = (int)dfk_cdiv(nwin, want);
@@ -3292,6 +3419,8 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     const bool want_drpb = a.rpb && bp->drpb;
     if (want_drpb && !bp->ws) return DFK_EINVAL;
     bf16raw* dsg = want_drpb ? reinterpret_cast<bf16raw*>(bp->ws) : nullptr;
+    const int G = bwd3_group(a, g);
+    const long slabw = bwd3_slab_windows(a, g, G);
 #define LAUNCH_B3(HD, TB, DR, CS)                                                                          \
   do {                                                                                                     \
     auto kfn = wattn_bwd3_kernel<HD, TB, DR, CS>;                                                            \
@@ -3301,8 +3430,8 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
       attr_set = true;                                                                                     \
     }                                                                                                      \
     for (int q0 = 0; q0 < g.Np; q0 += Qn)                                                                  \
-      hipLaunchKernelGGL(kfn, dim3((unsigned)units), dim3(64 * nw), lds, s, *bp, g, q0,                    \
-                         std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0, dsg, tb);                                \
+      hipLaunchKernelGGL(kfn, dim3((unsigned)(slabw * a.heads)), dim3(64 * nw), lds, s, *bp, g, q0,        \
+                         std::min(Qn, g.Np - q0), q0 > 0 ? 1 : 0, dsg, tb, G);                             \
   } while (0)
 #define PICK_B3(HD)                                                                            \
   do {                                                                                         \
@@ -3314,11 +3443,11 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
 #undef PICK_B3
 #undef LAUNCH_B3
     if (want_drpb) {
-      const DsPlan pl = ds_plan(a, g);
+      const DsPlan pl = ds_plan(a, g, slabw);
       float* rows = reinterpret_cast<float*>(reinterpret_cast<char*>(bp->ws) + ((pl.ds_elems * 2 + 15) & ~15L));
       hipLaunchKernelGGL(drpb_from_ds_kernel, dim3(pl.nchunks, a.heads, pl.nsplit), dim3(256),
-                         ((g.L + 3) & ~3) * 4, s, dsg, units, a.heads, g.Np, g.N, a.fh, a.fw, g.C0, g.L, pl.wps,
-                         rows);
+                         ((g.L + 3) & ~3) * 4, s, dsg, slabw * a.heads, a.heads, g.Np, g.N, a.fh, a.fw, g.C0, g.L,
+                         pl.wps, rows);
       hipLaunchKernelGGL(drpb_reduce_kernel, dim3(dfk_cdiv(g.L, 64), a.heads), dim3(1024), 0, s, rows, pl.rows,
                          a.heads, g.L, bp->drpb);
     }
@@ -3353,7 +3482,7 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
   } while (0)
     const bool want_drpb = a.rpb && bp->drpb;
     if (want_drpb && !bp->ws) return DFK_EINVAL;  // dRPB needs the dfk_wattn_bwd_workspace scratch
-    const DsPlan pl = ds_plan(a, g);
+    const DsPlan pl = ds_plan(a, g, units / a.heads);
     bf16raw* dsg = want_drpb ? reinterpret_cast<bf16raw*>(bp->ws) : nullptr;
     if (a.drop.mode) return DFK_EINVAL;   // attention dropout: v3 kernels only (as the forward)
     if (a.hd == 32) PICK_B16(32); else PICK_B16(64);
@@ -3411,8 +3540,15 @@ extern "C" int64_t dfk_wattn_bwd_workspace(const dfk_wattn_args* f) {
   const Geo g = make_geo(*f);
   const int64_t Lal = (g.L + 3) & ~3;
   if (f->dtype == DFK_BF16) {  // dS^T scratch (bf16) + per-block dRPB rows
-    const DsPlan pl = ds_plan(*f, g);
+    const bool v3 = !f->mask && f->scale > 0.f && f->tab;   // dfk_wattn_bwd's v3 path: grouped slabs
+    const DsPlan pl = ds_plan(*f, g, v3 ? bwd3_slab_windows(*f, g, bwd3_group(*f, g)) : (long)f->B * g.nW);
     return ((pl.ds_elems * 2 + 15) & ~15L) + pl.rows * Lal * 4;
   }
   return (int64_t)f->B * g.nW * f->heads * Lal * 4;  // fp32: one dRPB row per window-head
+}
+
+extern "C" int dfk_wattn_bwd_policy(int32_t group) {
+  if (group < 0 || group > 64) return DFK_EINVAL;
+  g_bwd_group = group;
+  return 0;
 }

@@ -371,12 +371,19 @@ def test_cosine_attention_logit_scale_dscore(heads, clamped, H):
     part = lambda t: t.permute(0, 1, 3, 5, 2, 4, 6).reshape(-1, heads, ws * ws, hd)
     q, k, v = part(q), part(k), part(v)
     s = torch.clamp(lr, max=max_log).exp()
-    attn = torch.nn.functional.normalize(q, dim=-1) @ torch.nn.functional.normalize(k, dim=-1).transpose(-1, -2)
-    attn = attn * s
+    # the kernels round q' = normalize(q) s and k' = normalize(k) to bf16 (CosineQKFn's output): the same rounding
+    # here, straight through (forward rounded, gradient of the unrounded map)
+    st = lambda t: t + (t.to(torch.bfloat16).double() - t).detach()
+    qn = st(torch.nn.functional.normalize(q, dim=-1) * s.view(1, heads, 1, 1))
+    kn = st(torch.nn.functional.normalize(k, dim=-1))
+    attn = qn @ kn.transpose(-1, -2)
     yy, xx = torch.meshgrid(torch.arange(ws), torch.arange(ws), indexing="ij")
     pos = (yy * (2 * ws - 1) + xx).flatten().to(DEV)
     idx = pos[:, None] - pos[None, :] + (ws - 1) * (2 * ws - 1) + (ws - 1)
-    attn = attn + tab.double()[idx].permute(2, 0, 1).unsqueeze(0)
+    # the kernels' bias tables hold bias * log2(e) in bf16 (wattn.hip, wattn_tab3_kernel): the same quantisation
+    l2e = 1.0 / math.log(2.0)
+    tq = (tab.double() * l2e).to(torch.bfloat16).double() / l2e
+    attn = attn + tq[idx].permute(2, 0, 1).unsqueeze(0)
     o = torch.softmax(attn, -1) @ v
     o = o.view(B, H // ws, W // ws, heads, ws, ws, hd).permute(0, 1, 4, 2, 5, 3, 6).reshape(rows, C)
     o.backward(dout.double())
@@ -385,10 +392,13 @@ def test_cosine_attention_logit_scale_dscore(heads, clamped, H):
     out_n, dl_n, dx_n = run(True)
     out_o, dl_o, dx_o = run(False)
     assert torch.equal(out_n, out_o)
-    assert torch.equal(dx_n, dx_o)   # the q / k / v gradients do not depend on where dlogit is taken
-    assert rel(out_n, o) < 2e-2
+    # the q / k / v gradients: the same arithmetic up to where the score's bias joins it (C input of the product,
+    # or added after it on the dscore path: fp32 rounding of S)
+    assert rel(dx_n, dx_o) < 1e-2
+    assert rel(out_n, o) < 5e-2   # scores up to s = 100: the bf16 Q' = q' log2(e) and bias tables quantise them
     err_n = ((dl_n.double() - ref).abs() / ref.abs().clamp_min(1e-30)).max().item()
     err_o = ((dl_o.double() - ref).abs() / ref.abs().clamp_min(1e-30)).max().item()
     print(f"logit_scale grad rel err: dscore {err_n:.3e}, q-hat.dq' {err_o:.3e}")
-    assert err_n < 1e-2
+    # both carry the kernels' bf16 rounding of Q' = q' log2(e) before the scores (a few % here, where the sum cancels)
+    assert err_n < 5e-2
     assert err_n <= err_o * 1.5 + 1e-4

@@ -191,3 +191,55 @@ def test_wattn_fwd_v5(case, extreme, policy):
     nW, N, Np = K.window_geometry(dims, window)
     d = (lse.view(-1, Np)[:, :N] - lse4.view(-1, Np)[:, :N]).abs().max().item()
     assert d < 1e-3 * max(1.0, lse4.view(-1, Np)[:, :N].abs().max().item()), d
+
+
+GROUP_CASES = [
+    ((4, 8, 14, 14), (8, 7, 7), (8, 7, 7), (4, 3, 3), 3, 32),   # 8 shift classes, ragged groups (2-window classes)
+    ((3, 4, 14, 14), (4, 7, 7), (4, 7, 7), (2, 3, 3), 2, 32),
+    ((5, 1, 14, 14), (1, 7, 7), (1, 7, 7), (0, 3, 3), 4, 32),   # SwinV2-shaped 49-token windows, 4 classes
+]
+
+
+@pytest.mark.parametrize("case", GROUP_CASES, ids=[str(i) for i in range(len(GROUP_CASES))])
+def test_wattn_bwd_grouped_drpb(case):
+    """The bf16 table backward with G windows of one (shift class, head) per workgroup summing their dS^T into one
+    dRPB scratch slab (dfk_wattn_bwd_policy): dq / dk / dv are bit-identical to the ungrouped launch (the same
+    arithmetic per window), dRPB within bf16 partial-sum rounding of it, and both match the fp32 reference."""
+    dims, window, fw, shift, heads, hd = case
+    g = torch.Generator(device=DEV).manual_seed(12)
+    rows = dims[0] * dims[1] * dims[2] * dims[3]
+    C = heads * hd
+    qkv = torch.randn(rows, 3 * C, device=DEV, generator=g).to(torch.bfloat16)
+    pads = [0.3 * torch.randn(C, device=DEV, generator=g).to(torch.bfloat16) for _ in range(3)]
+    Lt = (2 * fw[0] - 1) * (2 * fw[1] - 1) * (2 * fw[2] - 1)
+    rpb = torch.randn(Lt, heads, device=DEV, generator=g) * 0.5
+    scale = hd ** -0.5
+    out, lse, tab = K.wattn_fwd(qkv, qkv[:, C:], qkv[:, 2 * C:], 3 * C, dims, window, fw, shift, heads, hd, scale,
+                                rpb=rpb, pads=pads, return_table=True)
+    dout = torch.randn(rows, C, device=DEV, generator=g).to(torch.bfloat16)
+    res = {}
+    try:
+        for G in (1, 2, 3, 8):
+            K.wattn_bwd_policy(G)
+            dqkv = torch.empty_like(qkv)
+            drpb = torch.zeros(Lt, heads, device=DEV)
+            dpads = [torch.zeros(C, device=DEV) for _ in range(3)]
+            K.wattn_bwd((qkv, qkv[:, C:], qkv[:, 2 * C:], out, lse, 3 * C, dims, window, fw, shift, heads, hd, scale,
+                         rpb, pads), dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C, drpb=drpb, dpads=dpads, tab=tab)
+            res[G] = (dqkv, drpb, dpads)
+    finally:
+        K.wattn_bwd_policy(0)
+    torch.cuda.synchronize()
+    qr = qkv.float().requires_grad_(True)
+    rr = rpb.clone().requires_grad_(True)
+    ref = ref_attention(qr, [p.float() for p in pads], dims, window, fw, shift, heads, hd, scale, rr)
+    ref.backward(dout.float())
+    d1, r1, p1 = res[1]
+    for G, (dq, dr, dp) in res.items():
+        assert torch.equal(dq, d1), G
+        for a, b in zip(dp, p1):
+            assert torch.equal(a, b), G
+        e1 = ((dr - r1).abs().max() / r1.abs().max()).item()
+        assert e1 < 5e-3, (G, e1)
+        e = ((dr - rr.grad).abs().max() / rr.grad.abs().max()).item()
+        assert e < 3e-2, (G, e)

@@ -39,7 +39,11 @@ def timed(fn):
 
 def main():
     dt = torch.bfloat16
-    for name, dims, win, fw, shift, heads, hd, has_rpb in SHAPES + SHAPES[:1]:   # vst1 again, clocks warm
+    only = os.environ.get("WB_SHAPES")   # comma-separated name prefixes (profiling runs)
+    shapes = SHAPES + SHAPES[:1]   # vst1 again, clocks warm
+    if only:
+        shapes = [s for s in SHAPES if any(s[0].startswith(o) for o in only.split(","))]
+    for name, dims, win, fw, shift, heads, hd, has_rpb in shapes:
         rows = dims[0] * dims[1] * dims[2] * dims[3]
         C = heads * hd
         qkv = torch.randn(rows, 3 * C, device="cuda").to(dt)
