@@ -90,7 +90,7 @@ def time_kernel(fn, iters):
 
 
 ROOFLINE_KERNEL = "wattn_fwd6_kernel<false>"
-ROOFLINE_PMC = os.path.join(HERE, "profiles", "r5", "r5_wattn_fwd_pmc.json")   # tools/roofline_pmc.sh (round 5)
+ROOFLINE_PMC = os.path.join(HERE, "profiles", "r6", "r6_wattn_fwd_pmc.json")   # tools/gpu_round6.sh
 
 
 def stage1_geometry(cfg):
@@ -146,7 +146,7 @@ def pmc_traffic():
 
 
 CONV3D_KERNEL = "pe_fwd_kernel<6>"
-CONV3D_INSTEP = os.path.join(HERE, "profiles", "r5", "r5_conv3d_instep.json")   # tools/gpu_round5.sh
+CONV3D_INSTEP = os.path.join(HERE, "profiles", "r6", "r6_conv3d_instep.json")   # tools/gpu_round6.sh
 
 
 def conv3d_in_step():
@@ -191,13 +191,14 @@ def conv3d_roofline(cfg, B, iters, nbuf=3, instep=False):
             "in_step": conv3d_in_step() if instep else None}
 
 
-ATTN_BWD_KERNELS = "wattn_bwd3_kernel<32, true, false> + drpb_from_ds_kernel + drpb_reduce_kernel"
+ATTN_BWD_KERNELS = "wattn_bwd4_kernel + drpb_from_ds_kernel + drpb_reduce_kernel"
 
 
 def attn_bwd_roofline(cfg, B, dt, iters):
     """The stage-1 shifted-window attention BACKWARD of the same launch as `roofline` (WindowAttention3D.forward's
     autograd, video_swin_transformer.py:142-173): dQ, dK, dV and the relative-position-bias gradient dRPB, i.e.
-    the backward kernel plus the two dRPB launches (binning the dS scratch, reducing the partial rows).
+    the two-pass backward kernel (its dK/dV pass writes the window groups' summed dS^T slabs) plus the two dRPB
+    launches (binning the slabs, reducing the partial rows).
     Algorithmic FLOPs = 10 * window-heads * N^2 * hd (dP = dO V^T, dV = P^T dO, dS -> dQ = dS K, dK = dS^T Q, plus the
     recomputed S = Q K^T); the dRPB binning is counted as no FLOPs."""
     from deepfake_amd import kernels as K

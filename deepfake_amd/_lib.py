@@ -106,7 +106,7 @@ SIGNATURES = {
     "dfk_wattn_bwd": [C.POINTER(WattnBwdArgs), _VP],
     "dfk_wattn_bwd_workspace": [C.POINTER(WattnArgs)],
     "dfk_wattn_fwd_policy": [C.c_int32, C.c_int64],
-    "dfk_wattn_bwd_policy": [C.c_int32],
+    "dfk_wattn_bwd_policy": [C.c_int32, C.c_int32],
     "dfk_wattn_table_workspace": [C.POINTER(WattnArgs)],
     "dfk_wattn_table": [C.POINTER(WattnArgs), _VP],
     "dfk_patch_im2col": [_VP, C.c_int, _VP, C.c_int, C.POINTER(Im2colArgs), _VP],

@@ -1671,8 +1671,9 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // ONES (A/B, non-BAL only): the softmax denominators by a third PV-shaped MFMA with an all-ones A operand (every
 // output row = the column's sum of the bf16 P that also multiplies V) instead of 8 VALU adds per query half and
 // the lane-group sum at the store: -16 VALU adds per 32x32 block for +2 MFMAs on the matrix pipe, which has slack
-template <bool BAL, bool ONES = false>
-__global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args a, const Geo g, int qsplit,
+// W8 (A/B): up to 8 waves per workgroup (one query-block pair each) instead of 4 looping over the pairs
+template <bool BAL, bool ONES = false, bool W8 = false>
+__global__ __launch_bounds__(W8 ? 512 : 256, W8 ? 4 : 3) void wattn_fwd6_kernel(const dfk_wattn_args a, const Geo g, int qsplit,
                                                            const bf16raw* __restrict__ tab) {
   constexpr int HD = 32, CH = HD / 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1764,7 +1765,10 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh) lac[u][qh] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    for (int kb = k0; kb < k1; ++kb) {
+    // one key block; KH: the block's second 16 keys are all beyond N (the window's last block when N mod 32 is in
+    // (0, 16]: 392 = 12 x 32 + 8): their products, exponentials and P are skipped (P = 0 there anyway)
+    auto block = [&](int kb, auto kh_t) __attribute__((always_inline)) {
+      constexpr bool KH = decltype(kh_t)::value;
       const bf16raw* kbase = Ks + kb * 32 * HD;
       const bf16raw* vbase = Vs + kb * 32 * HD;
       bf16x8 kf[2];
@@ -1791,7 +1795,8 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
 #pragma unroll
       for (int u = 0; u < NC; ++u)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) d[u][t] = mfma16(kf[t & 1], qf[u][t >> 1], d[u][t]);
+        for (int t = 0; t < 4; ++t)
+          if (!KH || (t & 1) == 0) d[u][t] = mfma16(kf[t & 1], qf[u][t >> 1], d[u][t]);
       bf16x8 va[2];
 #pragma unroll
       for (int eh = 0; eh < 2; ++eh) va[eh] = tr16x2(vbase + vlo[eh], vbase + vhi[eh]);
@@ -1825,9 +1830,12 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             p[j] = __builtin_amdgcn_exp2f(d0[j]);
-            p[4 + j] = __builtin_amdgcn_exp2f(d1[j]);
+            p[4 + j] = KH ? 0.f : __builtin_amdgcn_exp2f(d1[j]);
           }
-          if constexpr (!ONES) ls[u][qh] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+          if constexpr (!ONES) {
+            if constexpr (KH) ls[u][qh] += (p[0] + p[1]) + (p[2] + p[3]);
+            else ls[u][qh] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+          }
           bf16x8 pv;
 #pragma unroll
           for (int j = 0; j < 8; ++j) pv[j] = (__bf16)p[j];
@@ -1842,7 +1850,13 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
           }
         }
       }
-    }
+    };
+    // the last block's second half is dead when N ends in its first half (SAFE keeps every block whole: its
+    // running maximum must see the -1e4 bias of dead keys exactly as before)
+    const bool tail_half = !SAFE && k1 == nkb && (nkb - 1) * 32 + 16 >= g.N;
+    const int kfull = tail_half ? k1 - 1 : k1;
+    for (int kb = k0; kb < kfull; ++kb) block(kb, std::false_type{});
+    if (tail_half) block(k1 - 1, std::true_type{});
     if constexpr (ONES) {
 #pragma unroll
       for (int u = 0; u < NC; ++u)
@@ -1903,13 +1917,19 @@ __global__ __launch_bounds__(256, 3) void wattn_fwd6_kernel(const dfk_wattn_args
     const int qb[2] = {qb0, min(qb1, nqb - 1)};
     bf16x8 qf[2][2];
     load_q(qb[0], qf[0]);
-    load_q(qb[1], qf[1]);
     f32x16 o[2];
     float ls[2][2], m[2][2];
     zero(o, ls, m);
-    chains(I2{}, FAST{}, qb, qf, 0, nkb, o, ls, m);
-    bool bad = store(qb[0], o[0], ls[0], m[0], true, ONES);
-    bad |= store(qb[1], o[1], ls[1], m[1], qb1 < nqb, ONES);
+    bool bad;
+    if (qb1 < nqb) {
+      load_q(qb[1], qf[1]);
+      chains(I2{}, FAST{}, qb, qf, 0, nkb, o, ls, m);
+      bad = store(qb[0], o[0], ls[0], m[0], true, ONES);
+      bad |= store(qb[1], o[1], ls[1], m[1], true, ONES);
+    } else {   // an odd block count's last block: one chain (it was computed twice, the copy discarded)
+      chains(I1{}, FAST{}, qb, qf, 0, nkb, o, ls, m);
+      bad = store(qb[0], o[0], ls[0], m[0], true, ONES);
+    }
     if (__builtin_amdgcn_ballot_w64(bad) != 0) {
       safe_block(qb[0]);
       if (qb1 < nqb) safe_block(qb1);
@@ -2085,6 +2105,7 @@ static long g_fwd_bal_min = getenv("DFK_WATTN_BALMIN") ? atol(getenv("DFK_WATTN_
 // gradient that cancels to a few % of its terms)
 static const int g_v6_min_qb = getenv("DFK_WATTN_V6MIN") ? atoi(getenv("DFK_WATTN_V6MIN")) : 4;   // A/B runs only
 static const int g_v6_ones = getenv("DFK_WATTN_ONES") ? atoi(getenv("DFK_WATTN_ONES")) : 0;      // A/B runs only
+static const int g_v6_w8 = getenv("DFK_WATTN_W8") ? atoi(getenv("DFK_WATTN_W8")) : 0;            // A/B runs only
 static bool use_v6(const dfk_wattn_args& a, const Geo& g) {
   return g_fwd_version == 6 && a.hd == 32 && !a.drop.mode && g.Np / 32 >= g_v6_min_qb;
 }
@@ -2144,7 +2165,8 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     static const int qgrp_env = getenv("DFK_WATTN_QB") ? atoi(getenv("DFK_WATTN_QB")) : 2;   // A/B runs only
     const int qgrp = tab && a.hd == 32 && !a.drop.mode && nqb >= 2 ? qgrp_env : 1;
     const int ngrp = dfk_cdiv(nqb, qgrp);
-    const int nw = std::min(4, ngrp);
+    const bool w8 = g_v6_w8 && tab && qgrp == 2 && use_v6(a, g);
+    const int nw = std::min(w8 ? 8 : 4, ngrp);
     int qsplit = (int)std::max<long>(1, std::min<long>(dfk_cdiv(ngrp, nw), dfk_cdiv(1024, units)));
     // v5 (no running max; A/B: DFK_WATTN_V=4 keeps v4) and its balanced schedule (one workgroup per unit, the
     // remaining pairs and the tail split by keys over the 4 waves) from DFK_WATTN_BALMIN units (default 512)
@@ -2152,7 +2174,7 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
     const bool v5 = tab && a.hd == 32 && !a.drop.mode && qgrp == 2 && g_fwd_version == 5;   // v4 otherwise
     const int pairs = nqb / 2;
     const long bal_min = g_fwd_bal_min >= 0 ? g_fwd_bal_min : (v5 ? 512 : LONG_MAX);
-    const bool bal = (v5 || v6) && nw == 4 && pairs % 4 != 3 && units >= bal_min;
+    const bool bal = (v5 || v6) && !w8 && nw == 4 && pairs % 4 != 3 && units >= bal_min;
     size_t lds_k = lds;
     if (bal) {
       qsplit = 1;
@@ -2174,6 +2196,7 @@ extern "C" int dfk_wattn_fwd(const dfk_wattn_args* ap, hipStream_t s) {
       if (tab) {
         if (a.drop.mode) LAUNCH_K((wattn_fwd4_kernel<32, true, 1>));
         else if (v6 && bal) LAUNCH_K((wattn_fwd6_kernel<true>));
+        else if (v6 && g_v6_w8) LAUNCH_K((wattn_fwd6_kernel<false, false, true>));
         else if (v6 && g_v6_ones) LAUNCH_K((wattn_fwd6_kernel<false, true>));
         else if (v6) LAUNCH_K((wattn_fwd6_kernel<false>));
         else if (bal) LAUNCH_K((wattn_fwd5_kernel<true>));
@@ -2894,8 +2917,33 @@ __device__ __forceinline__ float halving_sum16(float (&v)[16], int lane) {
   return v[0] + __shfl_xor(v[0], 1, 64);
 }
 
+// the same, with the 16 values produced on the fly by f(j) (the first halving step consumes them in pairs j,
+// j + 8: 8 live values instead of 16)
+template <typename F>
+__device__ __forceinline__ float halving_sum16_fn(F f, int lane) {
+  float v[8];
+  const bool lo16 = (lane & 16) == 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float a = f(i), b = f(8 + i);
+    v[i] = (lo16 ? a : b) + __shfl_xor(lo16 ? b : a, 16, 64);
+  }
+#pragma unroll
+  for (int st = 1; st < 4; ++st) {
+    const int n = 8 >> st, m = 16 >> st;
+    const bool lo = (lane & m) == 0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const float send = lo ? v[n + i] : v[i];
+      const float keep = lo ? v[i] : v[n + i];
+      v[i] = keep + __shfl_xor(send, m, 64);
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1, 64);
+}
+
 template <int HD, bool TAB, bool DROP, bool COS = false>
-__global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_args ba, const Geo g, int q0, int Qn,
+__global__ __launch_bounds__(COS ? 256 : 512) void wattn_bwd3_kernel(const dfk_wattn_bwd_args ba, const Geo g, int q0, int Qn,
                                                          int accum_kv, bf16raw* __restrict__ dsg,
                                                          const bf16raw* __restrict__ tabb, int G) {
   constexpr int NKK = HD / 16, NOT = HD / 32, CH = HD / 8;
@@ -3106,18 +3154,15 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
           }
         }
       float cosD = 0.f, cosB = 0.f;   // COS: this lane's row (register (r >> 1) & 15) sums over the block's keys
-      if constexpr (COS) {
-        float vd[16], vb[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float P = __builtin_amdgcn_exp2f(s[j]);
-          const float ds = P * dp[j];
+      if constexpr (COS) {   // the values produced as the halving consumes them (register pressure)
+        cosD = halving_sum16_fn([&](int j) __attribute__((always_inline)) {
+          const float ds = __builtin_amdgcn_exp2f(s[j]) * dp[j];
           accA += ds * raw[j];
-          vd[j] = ds;
-          vb[j] = P * raw[j];
-        }
-        cosD = halving_sum16(vd, lane);
-        cosB = halving_sum16(vb, lane);
+          return ds;
+        }, lane);
+        cosB = halving_sum16_fn([&](int j) __attribute__((always_inline)) {
+          return __builtin_amdgcn_exp2f(s[j]) * raw[j];
+        }, lane);
       }
       // dS^T -> the wave's scratch: registers 4v .. 4v+3 (queries 8v + 4hh + 0..3) at [key r][8v + 4hh]
 #pragma unroll
@@ -3263,6 +3308,415 @@ __global__ __launch_bounds__(512) void wattn_bwd3_kernel(const dfk_wattn_bwd_arg
   }
 }
 
+// ------------------------------------------------- v4 backward: two passes, no barriers in the main loops
+// One workgroup = G windows of one (shift class, head) in turn (decode_group); per window the prologue stages Q'
+// (= Q scale log2e), dO, K and V of the whole window in LDS (one image each, XOR-swizzled), -lse log2e and -delta
+// per query.  Then every wave takes work units on its own, with no barrier until the next window:
+//   pass A, unit = key block kb (keys on the lane, as wattn_bwd3): for every query block S = Q' K^T + bias' - L',
+//     dP = dO V^T - delta, P = 2^S, dS = P dP; dV^T += dO^T P, dK^T += Q'^T dS in registers; dS^T -> the dRPB slab.
+//   pass B, unit = query block qb (queries on the lane, the v6 forward's 16x16x32 sub-tiles and bias layout): for
+//     every key block S^T and dP^T the same way, dQ^T += K^T dS^T in registers (dS^T is the accumulator itself,
+//     in the PV slot order of the forward: no LDS transpose).
+// The score products run twice (S and dP in both passes: 14 instead of 10 MFMA-equivalents per block), in exchange
+// for no dQ reduction across waves, no per-step barrier and no dS LDS round trip — wattn_bwd3's staggered loop
+// spent most of each step waiting on those.  bf16 table path, hd 32, no dropout, windows of >= 4 query blocks (the
+// v6 forward's bias layout).
+constexpr int kB4Waves = 8;
+
+// Hand-counted buffer loads / stores for bwd4's pass A: the compiler's waitcnt placement put a vmcnt(0) at the top
+// of every step of a loop that mixes loads and stores (each step then waited for its predecessor's scratch stores
+// and read-modify-write loads to land), so the loop's memory operations are inline asm with explicit counts.  The
+// compiler does not count them: its own waits can only grow more conservative, never wrong.
+typedef int b4_v4i __attribute__((ext_vector_type(4)));
+typedef unsigned int b4_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int b4_u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ b4_v4i b4_rsrc(const void* base, int bytes) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base);
+  b4_v4i r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)p);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(p >> 32) & 0xffffu));   // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane(bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ b4_u32x4 b4_ld128(b4_v4i rs, uint32_t voff, int soff) {
+  b4_u32x4 d;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(rs), "s"(soff));
+  return d;
+}
+__device__ __forceinline__ b4_u32x2 b4_ld64(b4_v4i rs, uint32_t voff) {
+  b4_u32x2 d;
+  asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(d) : "v"(voff), "s"(rs));
+  return d;
+}
+__device__ __forceinline__ void b4_st64(b4_v4i rs, uint32_t voff, b4_u32x2 x) {
+  asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" : : "v"(x), "v"(voff), "s"(rs));
+}
+
+__global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_args ba, const Geo g,
+                                                         bf16raw* __restrict__ dsg, const bf16raw* __restrict__ tabf,
+                                                         const bf16raw* __restrict__ tabb, int G) {
+  constexpr int HD = 32, CH = HD / 8;
+  const dfk_wattn_args& a = ba.f;
+  const int Np = g.Np, nb = Np / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* p = smem;
+  bf16raw* Qs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;
+  bf16raw* dOs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;
+  bf16raw* Ks = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;
+  bf16raw* Vs = reinterpret_cast<bf16raw*>(p); p += 2 * (size_t)Np * HD;
+  int* trow = reinterpret_cast<int*>(p); p += 4 * Np;
+  float* nl2 = reinterpret_cast<float*>(p); p += 4 * Np;   // -lse log2e; -inf beyond N (P = 0)
+  float* ndl = reinterpret_cast<float*>(p); p += 4 * Np;   // -delta
+
+  const int tid = dfk_tid(), lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nw = dfk_bdim() >> 6;
+  const int r = lane & 31, hh = lane >> 5, g16 = lane >> 4, ql = lane & 15, tq = ql >> 2, tp = lane & 3;
+  const WGroup gr = decode_group(a, g, G);
+  const int head = gr.head, hoff = head * HD;
+  const float qs = a.scale * kLog2e;
+  // bias tiles (bwd layout for pass A, the v6 forward layout for pass B) through buffer descriptors
+  auto rsrc = [&](const bf16raw* base) __attribute__((always_inline)) {
+    const uint64_t t64 = reinterpret_cast<uint64_t>(base + ((long)gr.cls * a.heads + head) * (long)Np * Np);
+    const uint64_t tu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(t64 >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)t64);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(tu), (short)0, 0x7fffffff, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t trA = rsrc(tabb), trB = rsrc(tabf);
+  // the group's dS^T slab [k][q] through buffer descriptors, so no branch surrounds its loads and stores (a
+  // branch-guarded load got a vmcnt(0) right behind it): range 0 drops the stores / reads zeros
+  bf16raw* const dsu = dsg ? dsg + gr.slab * Np * Np : nullptr;
+  const int slab_bytes = __builtin_amdgcn_readfirstlane(dsu ? Np * Np * 2 : 0);
+  const uint64_t s64 = reinterpret_cast<uint64_t>(dsu ? dsu : reinterpret_cast<bf16raw*>(ba.dq));
+  const uint64_t su = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s64 >> 32)) << 32) |
+                      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s64);
+  const b4_v4i sst = b4_rsrc(reinterpret_cast<void*>(su), slab_bytes);
+  const b4_v4i tbA = b4_rsrc(tabb + ((long)gr.cls * a.heads + head) * (long)Np * Np, 0x7fffffff);
+
+  // per-lane LDS offsets (swz<32> depends on row bits 2-3 only: valid at any 32-row block offset)
+  int qoffA[2], tlo, thi, koffB[2], vlo[2], vhi[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) qoffA[kk] = swz<HD>(r, kk * 16 + hh * 8);
+  {
+    const int k0 = 4 * (g16 >> 1) + tq, col = 16 * (g16 & 1) + 4 * tp;
+    tlo = swz<HD>(k0, col);
+    thi = swz<HD>(k0 + 8, col);
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    koffB[h] = swz<HD>(16 * h + ql, 8 * g16);
+    vlo[h] = swz<HD>(4 * g16 + tq, 16 * h + 4 * tp);
+    vhi[h] = swz<HD>(16 + 4 * g16 + tq, 16 * h + 4 * tp);
+  }
+
+  for (int gi = 0; gi < gr.n; ++gi) {
+    const WUnit wu = group_window(a, g, gr, G, gi);
+    // later windows of the group add into what the first one stored
+    const b4_v4i sld = b4_rsrc(reinterpret_cast<void*>(su), gi > 0 ? slab_bytes : 0);
+    const long unit = wu.lse_unit;
+    for (int i = tid; i < Np; i += dfk_bdim()) {
+      trow[i] = token_info_row(a, g, wu.b, wu.win, i);
+      nl2[i] = i < g.N ? -a.lse[unit * Np + i] * kLog2e : -INFINITY;
+    }
+    __syncthreads();
+    // Q' / dO / O / K / V gather (all of a batch's loads issued before the wait that precedes their use)
+    {
+      constexpr int QB = 2;
+      const int tot = Np * CH;
+      for (int base = 0; base < tot; base += QB * dfk_bdim()) {
+        uint4 qv[QB], dv[QB], ov[QB], kv[QB], vv[QB];
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+          const int idx = min(base + u * (int)dfk_bdim() + tid, tot - 1);
+          const int li = idx / CH, c = (idx % CH) * 8;
+          const int row = trow[li];
+          qv[u] = tok_ld16<bf16raw>(a.q, a.pad_q, row, a.ld_qkv, hoff + c);
+          dv[u] = tok_ld16<bf16raw>(ba.dout, nullptr, row, ba.ld_dout, hoff + c);
+          ov[u] = tok_ld16<bf16raw>(a.out, nullptr, row, a.ld_out, hoff + c);
+          kv[u] = tok_ld16<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + c);
+          vv[u] = tok_ld16<bf16raw>(a.v, a.pad_v, row, a.ld_qkv, hoff + c);
+        }
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+          const int idx = base + u * (int)dfk_bdim() + tid;   // CH | blockDim: a row's CH lanes agree on idx < tot
+          float d = dot8_bf16(ov[u], dv[u]);
+#pragma unroll
+          for (int o = 1; o < CH; o <<= 1) d += __shfl_xor(d, o, 64);
+          if (idx < tot) {
+            const int li = idx / CH, c = (idx % CH) * 8;
+            bf16x8 qb8 = __builtin_bit_cast(bf16x8, qv[u]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qb8[j] = (__bf16)((float)qb8[j] * qs);   // the forward's Q' rounding
+            const int off = swz<HD>(li, c);
+            *reinterpret_cast<bf16x8*>(Qs + off) = qb8;
+            *reinterpret_cast<uint4*>(dOs + off) = dv[u];
+            *reinterpret_cast<uint4*>(Ks + off) = kv[u];
+            *reinterpret_cast<uint4*>(Vs + off) = vv[u];
+            if ((idx % CH) == 0) ndl[li] = -d;
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    for (int u = wave; u < 2 * nb; u += nw) {
+      if (u < nb) {
+        // ---------------- pass A: key block kb, keys on the lane (C layout: row q = 8v + 4hh + t, col key r)
+        const int kb = u;
+        const int krow = trow[kb * 32 + r];
+        bf16x8 kB[2], vB[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int off = kb * 32 * HD + qoffA[kk];
+          kB[kk] = *reinterpret_cast<const bf16x8*>(Ks + off);
+          vB[kk] = *reinterpret_cast<const bf16x8*>(Vs + off);
+        }
+        f32x16 dKt, dVt;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) { dKt[j] = 0.f; dVt[j] = 0.f; }
+        // per step i, in issue order: [wait bias(i)] bias(i+1) ... [wait old(i)] stores(i) old(i+1); so the bias of
+        // step i has the 8 operations of step i-1's tail younger than it, and old(i) the 2 bias loads of step i
+        b4_u32x4 bt0, bt1;
+        auto load_bias = [&](int qb) __attribute__((always_inline)) {
+          const int so = __builtin_amdgcn_readfirstlane((qb * nb + kb) * 2048);
+          bt0 = b4_ld128(tbA, lane * 16, so);
+          bt1 = b4_ld128(tbA, lane * 16 + 1024, so);
+        };
+        // slab tile (kb, qb): 2 KB at (kb nb + qb) 2048, [v][lane][4 queries] (drpb_from_ds_kernel tiled = 1)
+        const uint32_t srow = (uint32_t)(kb * nb * 2048 + lane * 8);
+        b4_u32x2 o0, o1, o2, o3;
+        auto load_old = [&](int qb) __attribute__((always_inline)) {
+          const uint32_t off = srow + 2048 * qb;
+          o0 = b4_ld64(sld, off);
+          o1 = b4_ld64(sld, off + 512);
+          o2 = b4_ld64(sld, off + 1024);
+          o3 = b4_ld64(sld, off + 1536);
+        };
+        // the next step's LDS operands (row constants, Q' / dO A fragments) are read during this step
+        f32x4 nlv[4], ndv[4];
+        bf16x8 qa[2], da[2];
+        auto load_rows = [&](int qb) __attribute__((always_inline)) {
+          const int qr0 = qb * 32;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            nlv[v] = *reinterpret_cast<const f32x4*>(nl2 + qr0 + 8 * v + 4 * hh);
+            ndv[v] = *reinterpret_cast<const f32x4*>(ndl + qr0 + 8 * v + 4 * hh);
+          }
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            const int off = qr0 * HD + qoffA[kk];
+            qa[kk] = *reinterpret_cast<const bf16x8*>(Qs + off);
+            da[kk] = *reinterpret_cast<const bf16x8*>(dOs + off);
+          }
+        };
+        int qb = (kb + wave) % nb;   // spread the waves' first query blocks
+        load_old(qb);
+        load_bias(qb);
+        load_rows(qb);
+        for (int i = 0; i < nb; ++i, qb = qb + 1 == nb ? 0 : qb + 1) {
+          const int qr0 = qb * 32, qbn = qb + 1 == nb ? 0 : qb + 1;
+          if (i == 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(bt0), "+v"(bt1));
+          else asm volatile("s_waitcnt vmcnt(8)" : "+v"(bt0), "+v"(bt1));
+          const bf16x8 bt[2] = {__builtin_bit_cast(bf16x8, bt0), __builtin_bit_cast(bf16x8, bt1)};
+          f32x16 s, dp;
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              s[4 * v + t] = nlv[v][t];
+              dp[4 * v + t] = ndv[v][t];
+            }
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const uint4 w4 = __builtin_bit_cast(uint4, bt[c]);
+            const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+            for (int i2 = 0; i2 < 4; ++i2) {
+              s[8 * c + 2 * i2] += __uint_as_float(w[i2] << 16);
+              s[8 * c + 2 * i2 + 1] += __uint_as_float(w[i2] & 0xffff0000u);
+            }
+          }
+          load_bias(qbn);
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            s = mfma32(qa[kk], kB[kk], s);
+            dp = mfma32(da[kk], vB[kk], dp);
+          }
+          load_rows(qbn);
+          bf16x8 pa[2], sa[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float P = __builtin_amdgcn_exp2f(s[8 * c + j]);
+              pa[c][j] = (__bf16)P;
+              sa[c][j] = (__bf16)(P * dp[8 * c + j]);
+            }
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int rb = (qr0 + 16 * c) * HD;
+            const bf16x8 doT = tr16x2(dOs + rb + tlo, dOs + rb + thi);
+            const bf16x8 qT = tr16x2(Qs + rb + tlo, Qs + rb + thi);
+            dVt = mfma32(doT, pa[c], dVt);
+            dKt = mfma32(qT, sa[c], dKt);
+          }
+          {   // dS^T[k][q] (+ the slab's earlier sum): sa[c] elements 4 (v & 1) .. 4 (v & 1) + 3 are queries 8 v + 4 hh ..
+            asm volatile("s_waitcnt vmcnt(2)" : "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
+            const b4_u32x2 old[4] = {o0, o1, o2, o3};
+            const uint32_t off = srow + 2048 * qb;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const uint4 u4 = __builtin_bit_cast(uint4, sa[v >> 1]);
+              const uint2 x = (v & 1) ? make_uint2(u4.z, u4.w) : make_uint2(u4.x, u4.y);
+              const uint2 y = add_bf16x4(x, make_uint2(old[v].x, old[v].y));   // + 0 for the group's first window
+              b4_st64(sst, off + 512 * v, b4_u32x2{y.x, y.y});
+            }
+            load_old(qbn);
+          }
+        }
+        // the last step's prefetches land in these registers: drain them before the registers are reused
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(bt0), "+v"(bt1), "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
+        // dK = (sum dS Q') ln 2, dV: lane holds key r, e = 8 v + 4 hh + t
+        const float kscale = 0.6931471805599453f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int e = hoff + 8 * v + 4 * hh;
+          if (krow >= 0) {
+            bf16raw* pk = reinterpret_cast<bf16raw*>(ba.dk) + (long)krow * ba.ld_dqkv + e;
+            bf16raw* pv = reinterpret_cast<bf16raw*>(ba.dv) + (long)krow * ba.ld_dqkv + e;
+            uint2 uk, uv;
+            uk.x = (uint32_t)f2bf(dKt[4 * v] * kscale) | ((uint32_t)f2bf(dKt[4 * v + 1] * kscale) << 16);
+            uk.y = (uint32_t)f2bf(dKt[4 * v + 2] * kscale) | ((uint32_t)f2bf(dKt[4 * v + 3] * kscale) << 16);
+            uv.x = (uint32_t)f2bf(dVt[4 * v]) | ((uint32_t)f2bf(dVt[4 * v + 1]) << 16);
+            uv.y = (uint32_t)f2bf(dVt[4 * v + 2]) | ((uint32_t)f2bf(dVt[4 * v + 3]) << 16);
+            *reinterpret_cast<uint2*>(pk) = uk;
+            *reinterpret_cast<uint2*>(pv) = uv;
+          } else if (krow == -1) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              if (ba.dpad_k) atomicAdd(ba.dpad_k + e + t, dKt[4 * v + t] * kscale);
+              if (ba.dpad_v) atomicAdd(ba.dpad_v + e + t, dVt[4 * v + t]);
+            }
+          }
+        }
+      } else {
+        // ---------------- pass B: query block qb, queries on the lane (v6 forward layout: sub-tile t = 2 qh + kh,
+        // lane (ql, g16) holds query 16 qh + ql, keys 16 kh + 4 g16 + 0..3)
+        const int qb = u - nb;
+        bf16x8 qf[2], df[2];
+        float nlq[2], ndq[2];
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const int q = qb * 32 + 16 * qh + ql;
+          const int off = swz<HD>(q, 8 * g16);
+          qf[qh] = *reinterpret_cast<const bf16x8*>(Qs + off);
+          df[qh] = *reinterpret_cast<const bf16x8*>(dOs + off);
+          nlq[qh] = nl2[q];
+          ndq[qh] = ndl[q];
+        }
+        f32x4 dq[2][2];
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+          for (int eh = 0; eh < 2; ++eh) dq[qh][eh] = f32x4{0.f, 0.f, 0.f, 0.f};
+        uint4 bt[2];
+        auto load_bias = [&](int kb) __attribute__((always_inline)) {
+          const int so = __builtin_amdgcn_readfirstlane((qb * nb + kb) * 2048);
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            bt[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(trB, lane * 16, so + c * 1024, 0));
+        };
+        // dead halves (all keys / all queries beyond N: the window's last block when N mod 32 is in (0, 16]) skip
+        // their products; their P (and so dS) is zero anyway
+        const bool qdead = qb * 32 + 16 >= g.N;
+        const int kdead_kb = (nb - 1) * 32 + 16 >= g.N ? nb - 1 : -1;
+        bf16x8 kf[2], vf[2], ka[2];   // the next key block's fragments are read during this step
+        auto load_kv = [&](int kb) __attribute__((always_inline)) {
+          const bf16raw* kbase = Ks + kb * 32 * HD;
+          const bf16raw* vbase = Vs + kb * 32 * HD;
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh) {
+            kf[kh] = *reinterpret_cast<const bf16x8*>(kbase + koffB[kh]);
+            vf[kh] = *reinterpret_cast<const bf16x8*>(vbase + koffB[kh]);
+          }
+#pragma unroll
+          for (int eh = 0; eh < 2; ++eh) ka[eh] = tr16x2(kbase + vlo[eh], kbase + vhi[eh]);
+        };
+        int kb = (qb + wave) % nb;
+        load_bias(kb);
+        load_kv(kb);
+        for (int i = 0; i < nb; ++i, kb = kb + 1 == nb ? 0 : kb + 1) {
+          const bool kdead = kb == kdead_kb;
+          const int kbn = kb + 1 == nb ? 0 : kb + 1;
+          f32x4 d[4], e[4];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {   // c = qh: element j of word i <-> key 16 (j >> 2) + 4 g16 + (j & 3)
+            const uint32_t w[4] = {bt[c].x, bt[c].y, bt[c].z, bt[c].w};
+#pragma unroll
+            for (int i2 = 0; i2 < 4; ++i2) {
+              d[2 * c + (i2 >> 1)][2 * (i2 & 1)] = __uint_as_float(w[i2] << 16) + nlq[c];
+              d[2 * c + (i2 >> 1)][2 * (i2 & 1) + 1] = __uint_as_float(w[i2] & 0xffff0000u) + nlq[c];
+            }
+            e[2 * c] = e[2 * c + 1] = f32x4{ndq[c], ndq[c], ndq[c], ndq[c]};
+          }
+          load_bias(kbn);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (((t & 1) && kdead) || ((t >> 1) && qdead)) continue;
+            d[t] = mfma16(kf[t & 1], qf[t >> 1], d[t]);
+            e[t] = mfma16(vf[t & 1], df[t >> 1], e[t]);
+          }
+          const bf16x8 kac[2] = {ka[0], ka[1]};
+          load_kv(kbn);
+#pragma unroll
+          for (int qh = 0; qh < 2; ++qh) {
+            if (qh == 1 && qdead) continue;
+            bf16x8 ds8;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              ds8[j] = (__bf16)(__builtin_amdgcn_exp2f(d[2 * qh][j]) * e[2 * qh][j]);
+              ds8[4 + j] = kdead ? (__bf16)0.f : (__bf16)(__builtin_amdgcn_exp2f(d[2 * qh + 1][j]) * e[2 * qh + 1][j]);
+            }
+#pragma unroll
+            for (int eh = 0; eh < 2; ++eh) dq[qh][eh] = mfma16(kac[eh], ds8, dq[qh][eh]);
+          }
+        }
+        // dQ = scale sum dS K: lane (ql, g16) of (qh, eh) holds query 16 qh + ql, e = 16 eh + 4 g16 + 0..3
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh) {
+          const int q = qb * 32 + 16 * qh + ql;
+          const int row = q < g.N ? trow[q] : -2;
+#pragma unroll
+          for (int eh = 0; eh < 2; ++eh) {
+            const int e = hoff + 16 * eh + 4 * g16;
+            if (row >= 0) {
+              uint2 w;
+              w.x = (uint32_t)f2bf(dq[qh][eh][0] * a.scale) | ((uint32_t)f2bf(dq[qh][eh][1] * a.scale) << 16);
+              w.y = (uint32_t)f2bf(dq[qh][eh][2] * a.scale) | ((uint32_t)f2bf(dq[qh][eh][3] * a.scale) << 16);
+              *reinterpret_cast<uint2*>(reinterpret_cast<bf16raw*>(ba.dq) + (long)row * ba.ld_dqkv + e) = w;
+            } else if (row == -1 && ba.dpad_q) {
+#pragma unroll
+              for (int t = 0; t < 4; ++t) atomicAdd(ba.dpad_q + e + t, dq[qh][eh][t] * a.scale);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();   // the next window of the group restages the LDS images
+  }
+}
+
+size_t bwd4_lds(const Geo& g) { return (size_t)g.Np * (8 * 32 + 12); }
+
+// the two-pass kernel's geometry (bf16 bias tables of the v6 forward layout, hd 32, no dropout); it alone groups
+// windows into shared dRPB slabs (wattn_bwd3's read-modify-write of the slab, behind a branch, stalled each step)
+extern int g_bwd_version;
+bool bwd4_geometry(const dfk_wattn_args& a, const Geo& g) {
+  return g_bwd_version == 4 && a.dtype == DFK_BF16 && !a.mask && a.scale > 0.f && a.tab && a.hd == 32 &&
+         !a.drop.mode && fwd16_layout(a, g) && bwd4_lds(g) <= 160 * 1024;
+}
+
 size_t bwd3_lds(const dfk_wattn_args& a, const Geo& g, int Qn, int nw, bool cos = false) {
   return 8 * (size_t)Qn * a.hd + 2 * (size_t)nw * 32 * kSdRow + 4 * (size_t)g.Np + 8 * (size_t)Qn +
          (cos ? 8 * (size_t)Qn + 64 : 0);
@@ -3271,9 +3725,12 @@ size_t bwd3_lds(const dfk_wattn_args& a, const Geo& g, int Qn, int nw, bool cos 
 // dRPB from the dS^T scratch: drpb[pos(q) - pos(k) + C0] += sum over windows of dS[q][k].
 // Block (chunk, head, split): 8 consecutive (k, q) elements per thread summed over the split's windows,
 // scattered into an LDS table (once per element per block), table -> one workspace row.
+// tiled = 0: a slab is dS^T [k][q] (wattn_bwd3); 1: 32 x 32 tiles (kb nb + qb) of 2 KB in the register order of
+// wattn_bwd4's dK/dV pass, [v][lane][t] with key 32 kb + (lane & 31), query 32 qb + 8 v + 4 (lane >> 5) + t (each
+// store instruction of that pass writes 512 contiguous bytes)
 __global__ __launch_bounds__(256) void drpb_from_ds_kernel(const bf16raw* __restrict__ ds, long units, int heads,
                                                            int Np, int N, int fh, int fw, int C0, int L, int wps,
-                                                           float* __restrict__ rows) {
+                                                           float* __restrict__ rows, int tiled) {
   extern __shared__ float tab[];
   const int chunk = dfk_bid_x(), h = dfk_bid_y(), split = dfk_bid_z();
   const int Lal = (L + 3) & ~3;
@@ -3316,13 +3773,28 @@ __global__ __launch_bounds__(256) void drpb_from_ds_kernel(const bf16raw* __rest
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += bf2f(pe[j]);
     }
-    const int k = (int)(e0 / Np), qb = (int)(e0 % Np);
-    if (k < N) {
-      auto pos = [&](int i) { return ((i / (fh * fw)) * (2 * fh - 1) + (i / fw) % fh) * (2 * fw - 1) + i % fw; };
-      const int pk = pos(k);
+    auto pos = [&](int i) { return ((i / (fh * fw)) * (2 * fh - 1) + (i / fw) % fh) * (2 * fw - 1) + i % fw; };
+    if (!tiled) {
+      const int k = (int)(e0 / Np), qb = (int)(e0 % Np);
+      if (k < N) {
+        const int pk = pos(k);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (qb + j < N) atomicAdd(tab + pos(qb + j) - pk + C0, acc[j]);
+        for (int j = 0; j < 8; ++j)
+          if (qb + j < N) atomicAdd(tab + pos(qb + j) - pk + C0, acc[j]);
+      }
+    } else {
+      const int nb = Np / 32, tile = (int)(e0 >> 10), w = (int)(e0 & 1023);
+      const int kb = tile / nb, qb = tile % nb, v = w >> 8, l0 = (w & 255) >> 2;
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) {
+        const int ln = l0 + hl, k = kb * 32 + (ln & 31), q0 = qb * 32 + 8 * v + 4 * (ln >> 5);
+        if (k < N) {
+          const int pk = pos(k);
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (q0 + t < N) atomicAdd(tab + pos(q0 + t) - pk + C0, acc[4 * hl + t]);
+        }
+      }
     }
   }
   __syncthreads();
@@ -3339,6 +3811,7 @@ struct DsPlan {
 // windows per backward work group (wattn_bwd3_kernel, decode_group): enough groups left for ~3 rounds of one
 // workgroup per CU (768), at most 8 (DFK_DRPB_G: A/B runs only)
 int g_bwd_group = getenv("DFK_DRPB_G") ? atoi(getenv("DFK_DRPB_G")) : 0;   // dfk_wattn_bwd_policy
+int g_bwd_version = getenv("DFK_WATTN_BWD") ? atoi(getenv("DFK_WATTN_BWD")) : 4;
 int bwd3_group(const dfk_wattn_args& a, const Geo& g) {
   if (g_bwd_group > 0) return g_bwd_group;
   const long units = (long)a.B * g.nW * a.heads;
@@ -3409,6 +3882,7 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     int nw = dfk_cdiv(nkb, dfk_cdiv(nkb, 8));   // passes of at most 8 waves, balanced
     const bool cos = bp->dscore != nullptr;
     if (cos && (!tab || a.drop.mode)) return DFK_EINVAL;   // dscore: the bias-table path without dropout only
+    if (cos) nw = std::min(nw, 4);   // its instantiation is bounded to 256 threads (the row sums' registers)
     int Qn = g.Np;                               // largest query chunk whose Q / dO / dQ fit the LDS ...
     while (Qn > 32 && bwd3_lds(a, g, Qn, nw, cos) > 160 * 1024) Qn -= 32;
     const int nch = dfk_cdiv(g.Np, Qn);          // ... then balanced chunks
@@ -3419,8 +3893,20 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     const bool want_drpb = a.rpb && bp->drpb;
     if (want_drpb && !bp->ws) return DFK_EINVAL;
     bf16raw* dsg = want_drpb ? reinterpret_cast<bf16raw*>(bp->ws) : nullptr;
-    const int G = bwd3_group(a, g);
+    const bool v4 = tab && bwd4_geometry(a, g);
+    if (v4 && cos) return DFK_EINVAL;   // dscore: the single-pass kernel (SwinV2's 49-token windows) only
+    const int G = v4 ? bwd3_group(a, g) : 1;
     const long slabw = bwd3_slab_windows(a, g, G);
+    if (v4) {   // the two-pass kernel (the v6 windows)
+      static bool attr4 = false;
+      if (!attr4) {
+        (void)hipFuncSetAttribute((const void*)wattn_bwd4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr4 = true;
+      }
+      hipLaunchKernelGGL(wattn_bwd4_kernel, dim3((unsigned)(slabw * a.heads)), dim3(64 * kB4Waves), bwd4_lds(g), s,
+                         *bp, g, dsg, tab3_fwd(a, g), tb, G);
+    }
 #define LAUNCH_B3(HD, TB, DR, CS)                                                                          \
   do {                                                                                                     \
     auto kfn = wattn_bwd3_kernel<HD, TB, DR, CS>;                                                            \
@@ -3439,7 +3925,9 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
     else if (tab) { if (a.drop.mode) LAUNCH_B3(HD, true, true, false); else LAUNCH_B3(HD, true, false, false); } \
     else { if (a.drop.mode) LAUNCH_B3(HD, false, true, false); else LAUNCH_B3(HD, false, false, false); }        \
   } while (0)
-    if (a.hd == 32) PICK_B3(32); else PICK_B3(64);
+    if (!v4) {
+      if (a.hd == 32) PICK_B3(32); else PICK_B3(64);
+    }
 #undef PICK_B3
 #undef LAUNCH_B3
     if (want_drpb) {
@@ -3447,7 +3935,7 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
       float* rows = reinterpret_cast<float*>(reinterpret_cast<char*>(bp->ws) + ((pl.ds_elems * 2 + 15) & ~15L));
       hipLaunchKernelGGL(drpb_from_ds_kernel, dim3(pl.nchunks, a.heads, pl.nsplit), dim3(256),
                          ((g.L + 3) & ~3) * 4, s, dsg, slabw * a.heads, a.heads, g.Np, g.N, a.fh, a.fw, g.C0, g.L,
-                         pl.wps, rows);
+                         pl.wps, rows, v4 ? 1 : 0);
       hipLaunchKernelGGL(drpb_reduce_kernel, dim3(dfk_cdiv(g.L, 64), a.heads), dim3(1024), 0, s, rows, pl.rows,
                          a.heads, g.L, bp->drpb);
     }
@@ -3492,7 +3980,7 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
       float* rows = reinterpret_cast<float*>(reinterpret_cast<char*>(bp->ws) + ((pl.ds_elems * 2 + 15) & ~15L));
       hipLaunchKernelGGL(drpb_from_ds_kernel, dim3(pl.nchunks, a.heads, pl.nsplit), dim3(256),
                          ((g.L + 3) & ~3) * 4, s, dsg, units, a.heads, g.Np, g.N, a.fh, a.fw, g.C0, g.L, pl.wps,
-                         rows);
+                         rows, 0);
       hipLaunchKernelGGL(drpb_reduce_kernel, dim3(dfk_cdiv(g.L, 64), a.heads), dim3(1024), 0, s, rows, pl.rows,
                          a.heads, g.L, bp->drpb);
     }
@@ -3540,15 +4028,16 @@ extern "C" int64_t dfk_wattn_bwd_workspace(const dfk_wattn_args* f) {
   const Geo g = make_geo(*f);
   const int64_t Lal = (g.L + 3) & ~3;
   if (f->dtype == DFK_BF16) {  // dS^T scratch (bf16) + per-block dRPB rows
-    const bool v3 = !f->mask && f->scale > 0.f && f->tab;   // dfk_wattn_bwd's v3 path: grouped slabs
-    const DsPlan pl = ds_plan(*f, g, v3 ? bwd3_slab_windows(*f, g, bwd3_group(*f, g)) : (long)f->B * g.nW);
+    const bool v4 = bwd4_geometry(*f, g);   // dfk_wattn_bwd's two-pass path: grouped slabs
+    const DsPlan pl = ds_plan(*f, g, v4 ? bwd3_slab_windows(*f, g, bwd3_group(*f, g)) : (long)f->B * g.nW);
     return ((pl.ds_elems * 2 + 15) & ~15L) + pl.rows * Lal * 4;
   }
   return (int64_t)f->B * g.nW * f->heads * Lal * 4;  // fp32: one dRPB row per window-head
 }
 
-extern "C" int dfk_wattn_bwd_policy(int32_t group) {
-  if (group < 0 || group > 64) return DFK_EINVAL;
+extern "C" int dfk_wattn_bwd_policy(int32_t group, int32_t version) {
+  if (group < 0 || group > 64 || (version != -1 && version != 3 && version != 4)) return DFK_EINVAL;
   g_bwd_group = group;
+  if (version > 0) g_bwd_version = version;
   return 0;
 }

@@ -428,7 +428,7 @@ def dscore_buffer(owner, qkv, heads, drop):
     dropout, the table path switched off): CosineQKFn then derives the logit_scale gradient from q-hat . dq'.
     Persistent per module (zeroed once; the consumer re-zeroes it), so a captured step holds no fill for it."""
     if qkv.dtype != torch.bfloat16 or drop is not None or os.environ.get("DFK_WATTN_TABLE", "1") == "0" \
-            or os.environ.get("DFK_COS_DSCORE", "1") == "0":
+            or os.environ.get("DFK_COS_DSCORE", "0") != "1":
         return None
     buf = getattr(owner, "_dfk_dscore", None)
     if buf is None or buf.device != qkv.device or buf.numel() != heads:

@@ -331,10 +331,11 @@ def wattn_fwd_policy(version=-1, bal_min_units=-1):
     L.check(L.lib().dfk_wattn_fwd_policy(int(version), int(bal_min_units)), "wattn_fwd_policy")
 
 
-def wattn_bwd_policy(group=0):
-    """Process-wide backward grouping (tests / A/B runs): windows per workgroup whose dS^T share one dRPB scratch
-    slab; 0 restores the automatic choice."""
-    L.check(L.lib().dfk_wattn_bwd_policy(int(group)), "wattn_bwd_policy")
+def wattn_bwd_policy(group=0, version=-1):
+    """Process-wide backward policy (tests / A/B runs): windows per workgroup whose dS^T share one dRPB scratch
+    slab (0 restores the automatic choice); version 4 (two-pass kernel, default) or 3 (staggered single pass),
+    -1 leaves it."""
+    L.check(L.lib().dfk_wattn_bwd_policy(int(group), int(version)), "wattn_bwd_policy")
 
 
 def wattn_bwd(fwd_args_tensors, dout, dq, dk, dv, ld_dqkv, drpb=None, dpads=None, mask=None, tab=None, drop=None,

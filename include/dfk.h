@@ -210,11 +210,13 @@ int dfk_wattn_fwd(const dfk_wattn_args* a, hipStream_t stream);
  * leaves a setting unchanged, bal_min_units -2 restores its default.  Returns 0.  dfk_wattn_table builds its forward bias tiles in
  * the layout of the version in force, so a table must come from the same policy as the forward that reads it. */
 int dfk_wattn_fwd_policy(int32_t version, int64_t bal_min_units);
-/* backward work grouping (process-wide; tests and A/B runs only): the bf16 table backward runs `group` windows of
+/* backward policy (process-wide; tests and A/B runs only).  group: the bf16 table backward runs `group` windows of
  * one (shift class, head) per workgroup and sums their dS^T into one dRPB scratch slab (0 = automatic: enough
- * groups for about three rounds of one workgroup per CU, at most 8).  dfk_wattn_bwd_workspace sizes for the
- * setting in force, so set it before asking for the workspace.  Returns 0, or DFK_EINVAL outside [0, 64]. */
-int dfk_wattn_bwd_policy(int32_t group);
+ * groups for about three rounds of one workgroup per CU, at most 8).  version: 4 = the two-pass kernel (dK/dV
+ * pass with keys on the lane, dQ pass with queries on the lane; hd 32 windows of >= 4 query blocks, the default),
+ * 3 = the staggered single-pass kernel everywhere, -1 leaves it.  dfk_wattn_bwd_workspace sizes for the setting
+ * in force, so set it before asking for the workspace.  Returns 0, or DFK_EINVAL. */
+int dfk_wattn_bwd_policy(int32_t group, int32_t version);
 int64_t dfk_wattn_table_workspace(const dfk_wattn_args* a);
 /* builds a->tab (fwd and bwd layouts) from a->rpb, the shift and the window geometry
  * (replaces the RPB gather + mask add of WindowAttention3D.forward, :152-163) */
