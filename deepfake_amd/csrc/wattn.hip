@@ -2892,10 +2892,11 @@ __device__ __forceinline__ int sd_off(int k, int q) { return k * kSdRow + ((((q 
 
 // two packed bf16 pairs + two packed bf16 pairs, fp32 add, round to nearest even
 __device__ __forceinline__ uint2 add_bf16x4(uint2 x, uint2 y) {
+  typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
   auto add2 = [](uint32_t p, uint32_t q) {
     const float lo = __uint_as_float(p << 16) + __uint_as_float(q << 16);
     const float hi = __uint_as_float(p & 0xffff0000u) + __uint_as_float(q & 0xffff0000u);
-    return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    return __builtin_bit_cast(uint32_t, bf16x2v{(__bf16)lo, (__bf16)hi});   // v_cvt_pk_bf16_f32 (RNE)
   };
   return make_uint2(add2(x.x, y.x), add2(x.y, y.y));
 }
@@ -2971,8 +2972,7 @@ __global__ __launch_bounds__(COS ? 256 : 512) void wattn_bwd3_kernel(const dfk_w
   const WGroup gr = decode_group(a, g, G);   // G windows of one (class, head), one dRPB scratch slab
   for (int gi = 0; gi < gr.n; ++gi) {
   float accA = 0.f;
-  const WUnit wu = group_window(a, g, gr, G, gi);   // lse / dropout rows by lse_unit
-  const bool rmw = gi > 0;                          // later windows add into the slab the first one stored
+  const WUnit wu = group_window(a, g, gr, G, gi);   // lse / dropout rows by lse_unit (the host runs G = 1 here)
   const int head = wu.head, win = wu.win, b = wu.b;
   const long unit = wu.lse_unit;
   const int hoff = head * HD;
@@ -3057,15 +3057,34 @@ __global__ __launch_bounds__(COS ? 256 : 512) void wattn_bwd3_kernel(const dfk_w
       kB[kk] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.k, a.pad_k, krow, a.ld_qkv, hoff + kk * 16 + hh * 8));
       vB[kk] = __builtin_bit_cast(bf16x8, tok_ld16<bf16raw>(a.v, a.pad_v, krow, a.ld_qkv, hoff + kk * 16 + hh * 8));
     }
+    {   // K as dQ's B operand (e on the lane): 16 NOT scattered 2-byte loads, all issued before any is used (one
+        // after another, each behind its own vmcnt(0), they cost a memory round trip apiece)
+      const bf16raw* kp[2][8][NOT];
+      bool kok[2][8];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int row = trow[kb * 32 + 16 * s + 8 * hh + j];
+        for (int j = 0; j < 8; ++j) {
+          const int row = trow[kb * 32 + 16 * s + 8 * hh + j];
 #pragma unroll
-        for (int ot = 0; ot < NOT; ++ot)
-          kN[s][ot][j] = __builtin_bit_cast(__bf16, tok_ld1<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + ot * 32 + r));
-      }
+          for (int ot = 0; ot < NOT; ++ot)
+            kp[s][j][ot] = tok_src<bf16raw>(a.k, a.pad_k, row, a.ld_qkv, hoff + ot * 32 + r, kok[s][j]);
+        }
+      bf16raw kv[2][8][NOT];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int ot = 0; ot < NOT; ++ot) kv[s][j][ot] = __builtin_nontemporal_load(kp[s][j][ot]);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int ot = 0; ot < NOT; ++ot)
+            kN[s][ot][j] = __builtin_bit_cast(__bf16, kok[s][j] ? kv[s][j][ot] : (bf16raw)0);
+    }
     f32x16 dKt[NOT], dVt[NOT];
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot)
@@ -3084,13 +3103,7 @@ __global__ __launch_bounds__(COS ? 256 : 512) void wattn_bwd3_kernel(const dfk_w
     load_bias(qb);
     for (int i = 0; i < nqb; ++i, qb = qb + 1 == nqb ? 0 : qb + 1) {
       const int qr0 = qb * 32;   // local row of the block in the chunk
-      // the slab's earlier sum of this tile (later windows of the group): loaded now, added at the store
       bf16raw* const gp = dsu ? dsu + (long)(kb * 32 + (lane >> 1)) * Np + q0 + qr0 + (lane & 1) * 16 : nullptr;
-      uint4 old0 = make_uint4(0, 0, 0, 0), old1 = old0;
-      if (dsu && rmw) {
-        old0 = *reinterpret_cast<const uint4*>(gp);
-        old1 = *reinterpret_cast<const uint4*>(gp + 8);
-      }
       // row constants as the C inputs: queries q0 + 8 v + 4 hh + (0..3) in registers 4v .. 4v+3
       f32x16 s, dp;
 #pragma unroll
@@ -3200,16 +3213,10 @@ __global__ __launch_bounds__(COS ? 256 : 512) void wattn_bwd3_kernel(const dfk_w
       }
       if (dsu) {   // scratch rows (32 keys x 64 B) -> global dS^T[k][q]: lane (key kr, half) un-swizzles 2 x 16 B
         const int kr = lane >> 1, half = lane & 1;
-        uint2 x0 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16));
-        uint2 x1 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 4));
-        uint2 x2 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 8));
-        uint2 x3 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 12));
-        if (rmw) {
-          x0 = add_bf16x4(x0, make_uint2(old0.x, old0.y));
-          x1 = add_bf16x4(x1, make_uint2(old0.z, old0.w));
-          x2 = add_bf16x4(x2, make_uint2(old1.x, old1.y));
-          x3 = add_bf16x4(x3, make_uint2(old1.z, old1.w));
-        }
+        const uint2 x0 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16));
+        const uint2 x1 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 4));
+        const uint2 x2 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 8));
+        const uint2 x3 = *reinterpret_cast<const uint2*>(Sw + sd_off(kr, half * 16 + 12));
 #ifdef DFK_DS_NT
         typedef unsigned int u32x4n __attribute__((ext_vector_type(4)));
         __builtin_nontemporal_store(u32x4n{x0.x, x0.y, x1.x, x1.y}, reinterpret_cast<u32x4n*>(gp));
@@ -3494,15 +3501,21 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
           o3 = b4_ld64(sld, off + 1536);
         };
         // the next step's LDS operands (row constants, Q' / dO A fragments) are read during this step
-        f32x4 nlv[4], ndv[4];
+        // (the row constants are read straight into the register order of the C input: no moves)
+        f32x16 nlv, ndv;
         bf16x8 qa[2], da[2];
         auto load_rows = [&](int qb) __attribute__((always_inline)) {
+          const float* pn = nl2 + qb * 32 + 4 * hh;
+          const float* pd = ndl + qb * 32 + 4 * hh;
           const int qr0 = qb * 32;
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            nlv[v] = *reinterpret_cast<const f32x4*>(nl2 + qr0 + 8 * v + 4 * hh);
-            ndv[v] = *reinterpret_cast<const f32x4*>(ndl + qr0 + 8 * v + 4 * hh);
-          }
+          nlv.s0123 = *reinterpret_cast<const f32x4*>(pn);
+          nlv.s4567 = *reinterpret_cast<const f32x4*>(pn + 8);
+          nlv.s89ab = *reinterpret_cast<const f32x4*>(pn + 16);
+          nlv.scdef = *reinterpret_cast<const f32x4*>(pn + 24);
+          ndv.s0123 = *reinterpret_cast<const f32x4*>(pd);
+          ndv.s4567 = *reinterpret_cast<const f32x4*>(pd + 8);
+          ndv.s89ab = *reinterpret_cast<const f32x4*>(pd + 16);
+          ndv.scdef = *reinterpret_cast<const f32x4*>(pd + 24);
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk) {
             const int off = qr0 * HD + qoffA[kk];
@@ -3510,7 +3523,7 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
             da[kk] = *reinterpret_cast<const bf16x8*>(dOs + off);
           }
         };
-        int qb = (kb + wave) % nb;   // spread the waves' first query blocks
+        int qb = __builtin_amdgcn_readfirstlane((kb + wave) % nb);   // spread the waves' first query blocks
         load_old(qb);
         load_bias(qb);
         load_rows(qb);
@@ -3519,14 +3532,11 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
           if (i == 0) asm volatile("s_waitcnt vmcnt(0)" : "+v"(bt0), "+v"(bt1));
           else asm volatile("s_waitcnt vmcnt(8)" : "+v"(bt0), "+v"(bt1));
           const bf16x8 bt[2] = {__builtin_bit_cast(bf16x8, bt0), __builtin_bit_cast(bf16x8, bt1)};
-          f32x16 s, dp;
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              s[4 * v + t] = nlv[v][t];
-              dp[4 * v + t] = ndv[v][t];
-            }
+          // S = Q'K^T - L' (the row constants as the C input), then + bias'; dP = dO V^T - delta
+          f32x16 s = mfma32(qa[0], kB[0], nlv), dp = mfma32(da[0], vB[0], ndv);
+          s = mfma32(qa[1], kB[1], s);
+          dp = mfma32(da[1], vB[1], dp);
+          load_rows(qbn);
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
             const uint4 w4 = __builtin_bit_cast(uint4, bt[c]);
@@ -3538,12 +3548,6 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
             }
           }
           load_bias(qbn);
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            s = mfma32(qa[kk], kB[kk], s);
-            dp = mfma32(da[kk], vB[kk], dp);
-          }
-          load_rows(qbn);
           bf16x8 pa[2], sa[2];
 #pragma unroll
           for (int c = 0; c < 2; ++c)
@@ -3603,9 +3607,10 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
       } else {
         // ---------------- pass B: query block qb, queries on the lane (v6 forward layout: sub-tile t = 2 qh + kh,
         // lane (ql, g16) holds query 16 qh + ql, keys 16 kh + 4 g16 + 0..3)
-        const int qb = u - nb;
+        const int qb = __builtin_amdgcn_readfirstlane(u - nb);
         bf16x8 qf[2], df[2];
-        float nlq[2], ndq[2];
+        float nlq[2];
+        f32x4 ndq4[2];   // -delta splat: the dP^T products' C input (loop invariant, no per-step moves)
 #pragma unroll
         for (int qh = 0; qh < 2; ++qh) {
           const int q = qb * 32 + 16 * qh + ql;
@@ -3613,7 +3618,8 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
           qf[qh] = *reinterpret_cast<const bf16x8*>(Qs + off);
           df[qh] = *reinterpret_cast<const bf16x8*>(dOs + off);
           nlq[qh] = nl2[q];
-          ndq[qh] = ndl[q];
+          const float nd = ndl[q];
+          ndq4[qh] = f32x4{nd, nd, nd, nd};
         }
         f32x4 dq[2][2];
 #pragma unroll
@@ -3627,10 +3633,6 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
           for (int c = 0; c < 2; ++c)
             bt[c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(trB, lane * 16, so + c * 1024, 0));
         };
-        // dead halves (all keys / all queries beyond N: the window's last block when N mod 32 is in (0, 16]) skip
-        // their products; their P (and so dS) is zero anyway
-        const bool qdead = qb * 32 + 16 >= g.N;
-        const int kdead_kb = (nb - 1) * 32 + 16 >= g.N ? nb - 1 : -1;
         bf16x8 kf[2], vf[2], ka[2];   // the next key block's fragments are read during this step
         auto load_kv = [&](int kb) __attribute__((always_inline)) {
           const bf16raw* kbase = Ks + kb * 32 * HD;
@@ -3643,11 +3645,10 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
 #pragma unroll
           for (int eh = 0; eh < 2; ++eh) ka[eh] = tr16x2(kbase + vlo[eh], kbase + vhi[eh]);
         };
-        int kb = (qb + wave) % nb;
+        int kb = __builtin_amdgcn_readfirstlane((qb + wave) % nb);
         load_bias(kb);
         load_kv(kb);
         for (int i = 0; i < nb; ++i, kb = kb + 1 == nb ? 0 : kb + 1) {
-          const bool kdead = kb == kdead_kb;
           const int kbn = kb + 1 == nb ? 0 : kb + 1;
           f32x4 d[4], e[4];
 #pragma unroll
@@ -3658,12 +3659,11 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
               d[2 * c + (i2 >> 1)][2 * (i2 & 1)] = __uint_as_float(w[i2] << 16) + nlq[c];
               d[2 * c + (i2 >> 1)][2 * (i2 & 1) + 1] = __uint_as_float(w[i2] & 0xffff0000u) + nlq[c];
             }
-            e[2 * c] = e[2 * c + 1] = f32x4{ndq[c], ndq[c], ndq[c], ndq[c]};
+            e[2 * c] = e[2 * c + 1] = ndq4[c];
           }
           load_bias(kbn);
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            if (((t & 1) && kdead) || ((t >> 1) && qdead)) continue;
             d[t] = mfma16(kf[t & 1], qf[t >> 1], d[t]);
             e[t] = mfma16(vf[t & 1], df[t >> 1], e[t]);
           }
@@ -3671,12 +3671,11 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
           load_kv(kbn);
 #pragma unroll
           for (int qh = 0; qh < 2; ++qh) {
-            if (qh == 1 && qdead) continue;
             bf16x8 ds8;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               ds8[j] = (__bf16)(__builtin_amdgcn_exp2f(d[2 * qh][j]) * e[2 * qh][j]);
-              ds8[4 + j] = kdead ? (__bf16)0.f : (__bf16)(__builtin_amdgcn_exp2f(d[2 * qh + 1][j]) * e[2 * qh + 1][j]);
+              ds8[4 + j] = (__bf16)(__builtin_amdgcn_exp2f(d[2 * qh + 1][j]) * e[2 * qh + 1][j]);
             }
 #pragma unroll
             for (int eh = 0; eh < 2; ++eh) dq[qh][eh] = mfma16(kac[eh], ds8, dq[qh][eh]);
