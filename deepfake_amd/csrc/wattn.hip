@@ -3813,8 +3813,11 @@ int g_bwd_group = getenv("DFK_DRPB_G") ? atoi(getenv("DFK_DRPB_G")) : 0;   // df
 int g_bwd_version = getenv("DFK_WATTN_BWD") ? atoi(getenv("DFK_WATTN_BWD")) : 4;
 int bwd3_group(const dfk_wattn_args& a, const Geo& g) {
   if (g_bwd_group > 0) return g_bwd_group;
+  // Step-level sweep (round 6, full training step, same box): G=8 280.0 clips/s, G=6 275.2, G=12 274.2,
+  // G=16 268.8, G=32 233.8, old auto rule (units/768, 4/2/1 per stage) 271.4. Fewer, longer
+  // workgroups overlap better with the branch streams than the isolated kernel time suggests.
   const long units = (long)a.B * g.nW * a.heads;
-  return (int)std::max<long>(1, std::min<long>(8, units / 768));
+  return (int)std::max<long>(1, std::min<long>(8, units / 64));
 }
 
 // dS^T slabs per head (window groups over the shift classes, as decode_group counts them)
