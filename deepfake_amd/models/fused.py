@@ -67,7 +67,8 @@ def build_fused(cfg, args=None, w2v_config=W2V_CONFIG, compute_dtype=torch.float
     m = FusionModel(args, VSTFeat(vst), mel, pa, out_dim=1, video_dim=cfg["video_dim"], audio_dim=cfg["audio_dim"],
                     paudio_dim=768)
     if fp8:   # C4: MX-fp8 video-trunk GEMMs (bf16 compute everywhere else)
-        set_fp8(m, cfg.get("fp8_stages", (2, 3)))
+        st = os.environ.get("DFK_FP8_STAGES")   # A/B knob: 0-based stages on MX-fp8, e.g. "2,3" (default) or "0,1,2,3"
+        set_fp8(m, tuple(int(v) for v in st.split(",") if v.strip()) if st is not None else cfg.get("fp8_stages", (2, 3)))
     return set_compute_dtype(m, compute_dtype)
 
 
