@@ -224,11 +224,21 @@ def attn_bwd_roofline(cfg, B, dt, iters):
     t = time_kernel(run, iters)
     flops = 10.0 * B * nW * heads * N * N * hd
     ach = flops / t / 1e12
+    # the same launch with 4 windows per workgroup (the isolated kernel's best; the step runs faster at the default 8,
+    # profiles/attn/r6_bwd4_group_sweep.txt) and without dRPB (the backward kernel alone, no slab writes)
+    K.wattn_bwd_policy(group=4)
+    try:
+        t4 = time_kernel(run, iters)
+    finally:
+        K.wattn_bwd_policy(group=0)
+    t0 = time_kernel(lambda: K.wattn_bwd(fa, dout, dqkv, dqkv[:, C:], dqkv[:, 2 * C:], 3 * C, drpb=None, tab=tab), iters)
     return {"kernel": ATTN_BWD_KERNELS + f" (stage-1 SW-MSA backward with dRPB, {N}-token windows, {heads} heads x "
             f"{hd}, {B * nW * heads} window-heads)", "bound": "mfma", "achieved": round(ach, 2),
             "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
             "flops_per_launch": flops, "avg_launch_ms": round(t * 1e3, 4),
-            "timing": f"HIP events over {iters} calls of the three launches"}
+            "group4": {"avg_launch_ms": round(t4 * 1e3, 4), "frac": round(flops / t4 / 1e12 / PEAK_BF16_TFLOPS, 4)},
+            "no_drpb": {"avg_launch_ms": round(t0 * 1e3, 4), "frac": round(flops / t0 / 1e12 / PEAK_BF16_TFLOPS, 4)},
+            "timing": f"HIP events over {iters} calls of the three launches (default: 8 windows per workgroup)"}
 
 
 def roofline(cfg, B, dt, iters, pmc=True):

@@ -928,7 +928,8 @@ void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int eve
   // weight gradients (k-major A: the token dimension is the reduction) on 128x128 tiles: tuning knob for their ring
   // depth (3 stages measured slower: dW 116 -> 119 us, C2 256.8 -> 247.7 clips/s, profiles/gemm/r4sdw_*)
   static const int sdw = getenv("DFK_DMA_SDW") ? atoi(getenv("DFK_DMA_SDW")) : 2;
-  const int st = g.a_kmajor && wt == 64 ? sdw : dma_stages(wt);
+  static const int sdw32 = getenv("DFK_DMA_SDW32") ? atoi(getenv("DFK_DMA_SDW32")) : 2;   // their 64x64 tiles (A/B)
+  const int st = g.a_kmajor && wt == 64 ? sdw : (g.a_kmajor && wt == 32 ? sdw32 : dma_stages(wt));
   if (wt == 33) {   // 128 x 64 (8 waves of 32 x 32)
     dispatch_dma_s<32, 4, 2, 2>(g, grid, kchunk, evec, sk, s);
     return;
@@ -942,6 +943,7 @@ void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int eve
     else dispatch_dma_s<64, 4, 2, 2>(g, grid, kchunk, evec, sk, s);
   } else if (wt == 64) {
     if (st == 2) dispatch_dma_s<64, 2, 2, 2>(g, grid, kchunk, evec, sk, s);
+    else if (st == 4) dispatch_dma_s<64, 2, 2, 4>(g, grid, kchunk, evec, sk, s);
     else dispatch_dma_s<64, 2, 2, 3>(g, grid, kchunk, evec, sk, s);
   } else {
     if (st == 2) dispatch_dma_s<32, 2, 2, 2>(g, grid, kchunk, evec, sk, s);
@@ -968,7 +970,10 @@ void dispatch(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int evec, S
 // wave tile: 64 (128 x 128 workgroup tiles) unless that grid has fewer than eight tiles per CU: then 32
 // (64 x 64 tiles, four times the workgroups, half the LDS, a 4-deep register ring of k-tiles in flight)
 int pick_wt(const dfk_gemm_args& g) {
-  if (g.atomic || g.splitk > 1) return 64;   // caller-planned split-K grids (weight gradients)
+  // caller-planned split-K grids (weight gradients): 128x128 tiles (A/B knob DFK_DW_WT=32: 64x64 tiles, whose
+  // smaller LDS stages let three workgroups per CU keep more bytes in flight)
+  static const int dw_wt = getenv("DFK_DW_WT") ? atoi(getenv("DFK_DW_WT")) : 64;
+  if (g.atomic || g.splitk > 1) return dw_wt == 32 ? 32 : 64;
   static const int force = getenv("DFK_GEMM_WT") ? atoi(getenv("DFK_GEMM_WT")) : 0;   // tuning runs only
   if (force == 32 || force == 64) return force;
   // measured on the C2 Linear shapes (tools/gemm_bench.py, both tile shapes): below 2048 128x128 tiles (eight
@@ -1272,16 +1277,35 @@ __global__ __launch_bounds__(256) void mx_quant_kernel(const T* __restrict__ x, 
   }
 }
 
-// x^T along x's rows: a 128 (r) x 64 (c) tile through LDS; output row c = 16 lanes x 8 consecutive r
+// x^T along x's rows: a 128 (r) x 64 (c) tile through LDS; output row c = 16 lanes x 8 consecutive r.
+// Full tiles (vec: 16-B aligned rows) load 8-element chunks, all four of a thread in flight at once (the
+// weights' dX operand: grids of 32-128 workgroups, so the per-workgroup latency is the kernel time; the
+// element-wise loop ran 17 us per Swin-B stage-3 weight); the column tail keeps the element-wise loop
 template <typename T>
 __global__ __launch_bounds__(256) void mx_quant_t_kernel(const T* __restrict__ x, int R, int C, long ldx,
-                                                         uint8_t* __restrict__ q, long ldq, uint32_t* __restrict__ s) {
+                                                         uint8_t* __restrict__ q, long ldq, uint32_t* __restrict__ s,
+                                                         int vec) {
   __shared__ float tile[128][65];
   const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 128, tid = threadIdx.x, lane = tid & 63;
+  if (vec && c0 + 64 <= C) {
+    float v[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + j * 256;
+      ld8<T>(x + (long)(r0 + (i >> 3)) * ldx + c0 + (i & 7) * 8, v[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + j * 256;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) tile[i >> 3][(i & 7) * 8 + e] = v[j][e];
+    }
+  } else {
 #pragma unroll 4
-  for (int i = tid; i < 128 * 64; i += 256) {
-    const int rr = i >> 6, cc = i & 63;
-    tile[rr][cc] = c0 + cc < C ? ldf<T>(x + (long)(r0 + rr) * ldx + c0 + cc) : 0.f;
+    for (int i = tid; i < 128 * 64; i += 256) {
+      const int rr = i >> 6, cc = i & 63;
+      tile[rr][cc] = c0 + cc < C ? ldf<T>(x + (long)(r0 + rr) * ldx + c0 + cc) : 0.f;
+    }
   }
   __syncthreads();
   const int ch = tid & 15;
@@ -1446,12 +1470,13 @@ extern "C" int dfk_mx_quant(const void* x, int dtype, int64_t rows, int64_t cols
     if (rows % 128 || ldq < rows || ldx < cols || rows > 0x7fffffff || cols > 0x7fffffff) return DFK_EINVAL;
     dim3 grid(dfk_cdiv(cols, 64), (unsigned)(rows / 128));
     if (grid.y > 65535) return DFK_EINVAL;
+    const int vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && ldx % 8 == 0;
     if (dtype == DFK_BF16)
       hipLaunchKernelGGL(mx_quant_t_kernel<bf16raw>, grid, dim3(256), 0, s, (const bf16raw*)x, (int)rows, (int)cols,
-                         (long)ldx, q, (long)ldq, sc);
+                         (long)ldx, q, (long)ldq, sc, vec);
     else
       hipLaunchKernelGGL(mx_quant_t_kernel<float>, grid, dim3(256), 0, s, (const float*)x, (int)rows, (int)cols,
-                         (long)ldx, q, (long)ldq, sc);
+                         (long)ldx, q, (long)ldq, sc, vec);
   }
   DFK_CHECK_LAUNCH();
   return 0;

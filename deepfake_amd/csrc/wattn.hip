@@ -3816,8 +3816,10 @@ int bwd3_group(const dfk_wattn_args& a, const Geo& g) {
   // Step-level sweep (round 6, full training step, same box): G=8 280.0 clips/s, G=6 275.2, G=12 274.2,
   // G=16 268.8, G=32 233.8, old auto rule (units/768, 4/2/1 per stage) 271.4. Fewer, longer
   // workgroups overlap better with the branch streams than the isolated kernel time suggests.
+  static const long minwg = getenv("DFK_DRPB_GMINWG") ? atol(getenv("DFK_DRPB_GMINWG")) : 64;   // A/B runs only
+  static const long gmax = getenv("DFK_DRPB_GMAX") ? atol(getenv("DFK_DRPB_GMAX")) : 8;         // A/B runs only
   const long units = (long)a.B * g.nW * a.heads;
-  return (int)std::max<long>(1, std::min<long>(8, units / 64));
+  return (int)std::max<long>(1, std::min<long>(gmax, units / std::max<long>(1, minwg)));
 }
 
 // dS^T slabs per head (window groups over the shift classes, as decode_group counts them)

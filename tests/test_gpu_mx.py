@@ -34,7 +34,7 @@ def test_mx_quant_bit_exact(shape, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("shape", [(128, 5), (256, 130), (512, 64)])
+@pytest.mark.parametrize("shape", [(128, 5), (256, 130), (512, 64), (1024, 512), (384, 200)])
 def test_mx_quant_transposed_bit_exact(shape, dtype):
     """x [R, C] -> the MX operand of x^T ([C, R], blocks along R): the dX GEMM's W^T."""
     from deepfake_amd import kernels as K

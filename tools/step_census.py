@@ -6,7 +6,9 @@ its launches/step overstates the step. This tool cuts the trace at the step's la
 `sgd_runs_kernel`) and reports, for the last N complete steps (the timed graph replays): launches per step,
 kernel time per step and per-kernel counts.
 
-    python tools/step_census.py run_kernel_trace.csv [N=5] [top=30]
+    python tools/step_census.py run_kernel_trace.csv [N=5] [top=30] [marker=sgd_runs_kernel]
+
+(marker: any kernel launched once per step, e.g. pe_bwd_kernel for builds before the one-launch SGD)
 """
 import collections
 import csv
@@ -18,14 +20,15 @@ def main():
     path = sys.argv[1]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 30
+    marker = sys.argv[4] if len(sys.argv) > 4 else "sgd_runs_kernel"
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    ends = [i for i, r in enumerate(rows) if "sgd_runs_kernel" in r[2]]
+    ends = [i for i, r in enumerate(rows) if marker in r[2]]
     if len(ends) < n + 1:
-        sys.exit(f"only {len(ends)} sgd_runs_kernel launches in the trace")
+        sys.exit(f"only {len(ends)} {marker} launches in the trace")
     steps = []
     for a, b in zip(ends[-n - 1:-1], ends[-n:]):
         seg = rows[a + 1:b + 1]

@@ -15,7 +15,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--top", type=int, default=40)
-    ap.add_argument("--end-kernel", default="sgd_kernel")
+    ap.add_argument("--end-kernel", default="sgd_runs_kernel")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]) for r in rows))
