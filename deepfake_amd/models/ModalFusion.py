@@ -5,6 +5,8 @@ The head runs on [B, <=1536] features: its Linear layers are the MFMA GEMM
 statistics, momentum 0.08) and sigmoid are latency-trivial torch ops.
 Extractor features arrive as fp32 [B, dim] whatever the trunk compute dtype.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -61,7 +63,10 @@ class FusionModel(nn.Module):
 
     def branch_streams(self):
         if not hasattr(self, "_streams"):
-            self._streams = [torch.cuda.Stream() for _ in range(3)]
+            # A/B knob: HIP stream priorities of the video / mel / waveform branches, e.g. "-1,0,0" (lower = higher)
+            pr = os.environ.get("DFK_BRANCH_PRIO")
+            ps = [int(v) for v in pr.split(",")] if pr else [0, 0, 0]
+            self._streams = [torch.cuda.Stream(priority=p) for p in ps]
         return self._streams
 
     def join_branches(self):

@@ -46,3 +46,5 @@ if [ "$6" == "c5" ]; then
 fi
 timeout -k 10 300 python3 -u tools/determinism_probe.py c2 bf16 2 > $OUT/determinism_c2_bf16.txt 2>&1 || { tail -20 $OUT/determinism_c2_bf16.txt; exit 1; }
 head -30 $OUT/determinism_c2_bf16.txt
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
+tail -3 $OUT/smoke.log
