@@ -930,12 +930,15 @@ void dispatch_dma(const dfk_gemm_args& g, int wt, dim3 grid, int kchunk, int eve
   static const int sdw = getenv("DFK_DMA_SDW") ? atoi(getenv("DFK_DMA_SDW")) : 2;
   static const int sdw32 = getenv("DFK_DMA_SDW32") ? atoi(getenv("DFK_DMA_SDW32")) : 2;   // their 64x64 tiles (A/B)
   const int st = g.a_kmajor && wt == 64 ? sdw : (g.a_kmajor && wt == 32 ? sdw32 : dma_stages(wt));
+  static const int s8w = getenv("DFK_DMA_S8W") ? atoi(getenv("DFK_DMA_S8W")) : 2;   // A/B: ring depth of the 8-wave tiles
   if (wt == 33) {   // 128 x 64 (8 waves of 32 x 32)
-    dispatch_dma_s<32, 4, 2, 2>(g, grid, kchunk, evec, sk, s);
+    if (s8w == 3) dispatch_dma_s<32, 4, 2, 3>(g, grid, kchunk, evec, sk, s);
+    else dispatch_dma_s<32, 4, 2, 2>(g, grid, kchunk, evec, sk, s);
     return;
   }
   if (wt == 34) {   // 64 x 128
-    dispatch_dma_s<32, 2, 4, 2>(g, grid, kchunk, evec, sk, s);
+    if (s8w == 3) dispatch_dma_s<32, 2, 4, 3>(g, grid, kchunk, evec, sk, s);
+    else dispatch_dma_s<32, 2, 4, 2>(g, grid, kchunk, evec, sk, s);
     return;
   }
   if (wt == 128) {
