@@ -3330,6 +3330,14 @@ __global__ __launch_bounds__(COS ? 256 : 512) void wattn_bwd3_kernel(const dfk_w
 // v6 forward's bias layout).
 constexpr int kB4Waves = 8;
 
+// Which work units (pass-A key blocks 0..nb-1, pass-B query blocks nb..2nb-1) each wave of a bwd4 workgroup runs:
+// byte w (w <= kB4Waves) = the first list position of wave w, the unit list from byte 16 on.  Round robin
+// (u = wave, wave + 8, ...) gives a 392-token window's 26 units to the 8 waves as 4/4/3/.../3; the host plans a
+// longest-processing-time assignment instead (a pass-A step runs 4 products, a pass-B step 3): makespan 12 against
+// 14 such products per window.
+struct B4Sched { uint32_t w[16]; };
+__device__ __forceinline__ int b4_sched_byte(const B4Sched& sc, int i) { return (sc.w[i >> 2] >> (8 * (i & 3))) & 0xff; }
+
 // Hand-counted buffer loads / stores for bwd4's pass A: the compiler's waitcnt placement put a vmcnt(0) at the top
 // of every step of a loop that mixes loads and stores (each step then waited for its predecessor's scratch stores
 // and read-modify-write loads to land), so the loop's memory operations are inline asm with explicit counts.  The
@@ -3363,7 +3371,7 @@ __device__ __forceinline__ void b4_st64(b4_v4i rs, uint32_t voff, b4_u32x2 x) {
 
 __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_args ba, const Geo g,
                                                          bf16raw* __restrict__ dsg, const bf16raw* __restrict__ tabf,
-                                                         const bf16raw* __restrict__ tabb, int G) {
+                                                         const bf16raw* __restrict__ tabb, int G, const B4Sched sched) {
   constexpr int HD = 32, CH = HD / 8;
   const dfk_wattn_args& a = ba.f;
   const int Np = g.Np, nb = Np / 32;
@@ -3467,7 +3475,10 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
     }
     __syncthreads();
 
-    for (int u = wave; u < 2 * nb; u += nw) {
+    const int us0 = __builtin_amdgcn_readfirstlane(b4_sched_byte(sched, wave));
+    const int us1 = __builtin_amdgcn_readfirstlane(b4_sched_byte(sched, wave + 1));
+    for (int ui = us0; ui < us1; ++ui) {
+      const int u = __builtin_amdgcn_readfirstlane(b4_sched_byte(sched, 16 + ui));
       if (u < nb) {
         // ---------------- pass A: key block kb, keys on the lane (C layout: row q = 8v + 4hh + t, col key r)
         const int kb = u;
@@ -3713,7 +3724,7 @@ size_t bwd4_lds(const Geo& g) { return (size_t)g.Np * (8 * 32 + 12); }
 extern int g_bwd_version;
 bool bwd4_geometry(const dfk_wattn_args& a, const Geo& g) {
   return g_bwd_version == 4 && a.dtype == DFK_BF16 && !a.mask && a.scale > 0.f && a.tab && a.hd == 32 &&
-         !a.drop.mode && fwd16_layout(a, g) && bwd4_lds(g) <= 160 * 1024;
+         !a.drop.mode && fwd16_layout(a, g) && bwd4_lds(g) <= 160 * 1024 && 2 * (g.Np / 32) <= 48;   // B4Sched
 }
 
 size_t bwd3_lds(const dfk_wattn_args& a, const Geo& g, int Qn, int nw, bool cos = false) {
@@ -3811,6 +3822,63 @@ struct DsPlan {
 // workgroup per CU (768), at most 8 (DFK_DRPB_G: A/B runs only)
 int g_bwd_group = getenv("DFK_DRPB_G") ? atoi(getenv("DFK_DRPB_G")) : 0;   // dfk_wattn_bwd_policy
 int g_bwd_version = getenv("DFK_WATTN_BWD") ? atoi(getenv("DFK_WATTN_BWD")) : 4;
+// bwd4's unit assignment (B4Sched): the smallest makespan over the waves for unit costs cA (a pass-A key block) and
+// cB (a pass-B query block) — units of one pass are interchangeable, so a plan is a count (a_w, b_w) per wave, found by
+// a DP per candidate makespan (DFK_B4_SCHED=0: round robin; DFK_B4_COST="cA,cB", default 4,3 products per step)
+B4Sched b4_sched(int nb) {
+  static const int mode = getenv("DFK_B4_SCHED") ? atoi(getenv("DFK_B4_SCHED")) : 1;   // A/B runs only
+  static int cA = 4, cB = 3;
+  static const bool parsed = [] {
+    if (const char* e = getenv("DFK_B4_COST")) {
+      int x = 0, y = 0;
+      if (sscanf(e, "%d,%d", &x, &y) == 2 && x > 0 && y > 0) { cA = x; cB = y; }
+    }
+    return true;
+  }();
+  (void)parsed;
+  constexpr int W = kB4Waves;
+  int na[W] = {}, nbw[W] = {};
+  if (mode == 0) {
+    for (int u = 0; u < 2 * nb; ++u) (u < nb ? na : nbw)[u % W] += 1;
+  } else {
+    // smallest T such that W waves hold nb A units and nb B units with cA a_w + cB b_w <= T
+    for (int T = ((nb * (cA + cB)) + W - 1) / W;; ++T) {
+      int cap[W + 1][64];   // cap[w][a] = max B units the first w waves hold with a A units among them (-1: none)
+      for (int w = 0; w <= W; ++w)
+        for (int a = 0; a <= nb; ++a) cap[w][a] = -1;
+      cap[0][0] = 0;
+      for (int w = 0; w < W; ++w)
+        for (int a = 0; a <= nb; ++a) {
+          if (cap[w][a] < 0) continue;
+          for (int x = 0; a + x <= nb && cA * x <= T; ++x)
+            cap[w + 1][a + x] = std::max(cap[w + 1][a + x], cap[w][a] + (T - cA * x) / cB);
+        }
+      if (cap[W][nb] < nb) continue;
+      // walk back: choose a_w per wave (any choice that keeps the rest feasible), b_w greedily
+      int a = nb, b = nb;
+      for (int w = W - 1; w >= 0; --w) {
+        for (int x = 0; x <= a && cA * x <= T; ++x) {
+          const int prev = cap[w][a - x];
+          if (prev < 0) continue;
+          const int take = std::min(b, (T - cA * x) / cB);
+          if (prev >= b - take) { na[w] = x; nbw[w] = take; a -= x; b -= take; break; }
+        }
+      }
+      break;
+    }
+  }
+  B4Sched sc{};
+  uint8_t* by = reinterpret_cast<uint8_t*>(sc.w);
+  int pos = 0, ua = 0, ub = nb;
+  for (int w = 0; w < W; ++w) {
+    by[w] = (uint8_t)pos;
+    for (int i = 0; i < na[w]; ++i) by[16 + pos++] = (uint8_t)ua++;
+    for (int i = 0; i < nbw[w]; ++i) by[16 + pos++] = (uint8_t)ub++;
+  }
+  by[W] = (uint8_t)pos;
+  return sc;
+}
+
 int bwd3_group(const dfk_wattn_args& a, const Geo& g) {
   if (g_bwd_group > 0) return g_bwd_group;
   // Step-level sweep (round 6, full training step, same box): G=8 280.0 clips/s, G=6 275.2, G=12 274.2,
@@ -3909,7 +3977,7 @@ extern "C" int dfk_wattn_bwd(const dfk_wattn_bwd_args* bp, hipStream_t s) {
         attr4 = true;
       }
       hipLaunchKernelGGL(wattn_bwd4_kernel, dim3((unsigned)(slabw * a.heads)), dim3(64 * kB4Waves), bwd4_lds(g), s,
-                         *bp, g, dsg, tab3_fwd(a, g), tb, G);
+                         *bp, g, dsg, tab3_fwd(a, g), tb, G, b4_sched(g.Np / 32));
     }
 #define LAUNCH_B3(HD, TB, DR, CS)                                                                          \
   do {                                                                                                     \
