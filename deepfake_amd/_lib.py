@@ -114,6 +114,8 @@ SIGNATURES = {
     "dfk_rowmean": [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP],
     "dfk_cast": [_VP, C.c_int, _VP, C.c_int, _I64, _VP],
     "dfk_gelu_bwd": [_VP, _VP, _VP, _I64, C.c_int, _VP],
+    "dfk_posconv_wnorm_fwd": [_VP, _VP, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP, _VP, C.c_int, _VP],
+    "dfk_posconv_wnorm_bwd": [_VP, _VP, _VP, _VP, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP, _VP],
     "dfk_cosine_qk_fwd": [_VP, _VP, _VP, _F, _I64, C.c_int, C.c_int, C.c_int, _VP],
     "dfk_cosine_qk_bwd": [_VP, _VP, _VP, _VP, _F, _VP, _I64, C.c_int, C.c_int, C.c_int, _VP, _VP],
     "dfk_cpb_bias_fwd": [_VP, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _VP],

@@ -576,3 +576,128 @@ extern "C" int dfk_sgd_step_runs(float* param, const float* grad, float* momentu
   DFK_CHECK_LAUNCH();
   return 0;
 }
+
+// ---- wav2vec2 positional-conv weight norm (HF weight_norm(dim=2), modeling_wav2vec2.py:336-350) ----
+// v [C][Cg][k] fp32, g [k]: w = g v / ||v[:, :, kk]||.  The forward writes w straight into the two GEMM operand
+// layouts the conv uses (w2: forward, w3: the transposed conv of its input gradient); the backward turns the dW GEMM's
+// fp32 output (w2's layout) into dv / dg.  Each workgroup owns one output row of C (its Cg x k slice, 24 KB at the
+// wav2vec2-base shape, staged in LDS so both the [Cg][k] and the [k][Cg] walks are coalesced); the per-kk sums go
+// through [C][k] partials and one fixed-order reduce (deterministic).
+namespace {
+
+// part[o][kk] = sum_i v[o][i][kk]^2 (dw2 == nullptr) or sum_i v[o][i][kk] dw[o][i][kk], dw[o][i][kk] = dw2[o][kk*Cg+i]
+__global__ __launch_bounds__(256) void wn_partial_kernel(const float* __restrict__ v, const float* __restrict__ dw2,
+                                                         int Cg, int k, float* __restrict__ part) {
+  extern __shared__ float wsm[];   // dw2 row o (k * Cg)
+  const int o = blockIdx.x, n = Cg * k;
+  const float* vo = v + (long)o * n;
+  if (dw2) {
+    for (int p = threadIdx.x; p < n; p += blockDim.x) wsm[p] = dw2[(long)o * n + p];
+    __syncthreads();
+  }
+  for (int kk = threadIdx.x; kk < k; kk += blockDim.x) {
+    float s = 0.f;
+    for (int i = 0; i < Cg; ++i) {
+      const float x = vo[i * k + kk];
+      s += dw2 ? x * wsm[kk * Cg + i] : x * x;
+    }
+    part[(long)o * k + kk] = s;
+  }
+}
+
+// fwd (dg == nullptr): norm[kk] = sqrt(sum_o part[o][kk]); bwd: dg[kk] += (sum_o part[o][kk]) / norm[kk], and the sum
+// itself is left in part[0][kk] for the dv pass.  One workgroup per kk: 256 strided partial sums, then a fixed-order
+// tree in LDS (one thread per kk walking all C partials took 170 us)
+__global__ __launch_bounds__(256) void wn_reduce_kernel(float* __restrict__ part, int C, int k, float* __restrict__ norm,
+                                                        float* __restrict__ dg) {
+  __shared__ float red[256];
+  const int kk = blockIdx.x, t = threadIdx.x;
+  float s = 0.f;
+  for (int o = t; o < C; o += 256) s += part[(long)o * k + kk];
+  red[t] = s;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (t < h) red[t] += red[t + h];
+    __syncthreads();
+  }
+  if (t == 0) {
+    const float tot = red[0];
+    if (dg) {
+      dg[kk] += tot / norm[kk];
+      part[kk] = tot;   // part[0][kk]: every workgroup has read its own column before this write (same kk only)
+    } else {
+      norm[kk] = sqrtf(tot);
+    }
+  }
+}
+
+// blockIdx.y 0: w2 row o = blockIdx.x, w2[o][kk*Cg+i] = g v[o][i][kk] / norm; 1: w3 row r = gr*Cg+ci,
+// w3[r][u*Cg+co] = w[gr*Cg+co][ci][k-1-u]
+template <typename T>
+__global__ __launch_bounds__(256) void wn_apply_fwd_kernel(const float* __restrict__ v, const float* __restrict__ g,
+                                                           const float* __restrict__ norm, int Cg, int k,
+                                                           T* __restrict__ w2, T* __restrict__ w3) {
+  extern __shared__ float vsm[];   // [Cg][k]: v[o] (w2) or v[gr*Cg+co][ci][:] for co = 0..Cg-1 (w3)
+  const int row = blockIdx.x, n = Cg * k;
+  const bool t3 = blockIdx.y == 1;
+  const int gr = row / Cg, ci = row % Cg;
+  for (int p = threadIdx.x; p < n; p += blockDim.x) {
+    const int a = p / k, kk = p % k;   // a = i (w2) or co (w3)
+    const long src = t3 ? ((long)(gr * Cg + a) * Cg + ci) * k + kk : (long)row * n + p;
+    vsm[p] = v[src] * (g[kk] / norm[kk]);
+  }
+  __syncthreads();
+  T* out = (t3 ? w3 : w2) + (long)row * n;
+  for (int p = threadIdx.x; p < n; p += blockDim.x) {
+    const int u = p / Cg, a = p % Cg;
+    stf<T>(out + p, t3 ? vsm[a * k + (k - 1 - u)] : vsm[a * k + u]);
+  }
+}
+
+// dv[o][i][kk] += g/norm dw - g s / norm^3 v  (s = part[0][kk] from wn_reduce_kernel)
+__global__ __launch_bounds__(256) void wn_apply_bwd_kernel(const float* __restrict__ v, const float* __restrict__ g,
+                                                           const float* __restrict__ norm, const float* __restrict__ s,
+                                                           const float* __restrict__ dw2, int Cg, int k,
+                                                           float* __restrict__ dv) {
+  extern __shared__ float wsm[];   // dw2 row o
+  const int o = blockIdx.x, n = Cg * k;
+  for (int p = threadIdx.x; p < n; p += blockDim.x) wsm[p] = dw2[(long)o * n + p];
+  __syncthreads();
+  for (int p = threadIdx.x; p < n; p += blockDim.x) {
+    const int i = p / k, kk = p % k;
+    const float nk = norm[kk], gk = g[kk];
+    dv[(long)o * n + p] += gk / nk * wsm[kk * Cg + i] - gk * s[kk] / (nk * nk * nk) * v[(long)o * n + p];
+  }
+}
+
+}  // namespace
+
+extern "C" int dfk_posconv_wnorm_fwd(const float* v, const float* g, int32_t C, int32_t Cg, int32_t k, float* norm,
+                                     float* ws, void* w2, void* w3, int dtype, hipStream_t s) {
+  if (!v || !g || !norm || !ws || !w2 || !w3 || C <= 0 || Cg <= 0 || k <= 0 || C % Cg) return DFK_EINVAL;
+  if (dtype != DFK_BF16 && dtype != DFK_F32) return DFK_EINVAL;
+  const size_t lds = sizeof(float) * (size_t)Cg * k;
+  if (lds > 64 * 1024) return DFK_EINVAL;
+  hipLaunchKernelGGL(wn_partial_kernel, dim3(C), dim3(256), 0, s, v, nullptr, Cg, k, ws);
+  hipLaunchKernelGGL(wn_reduce_kernel, dim3(k), dim3(256), 0, s, ws, C, k, norm, nullptr);
+  if (dtype == DFK_BF16)
+    hipLaunchKernelGGL(wn_apply_fwd_kernel<bf16raw>, dim3(C, 2), dim3(256), lds, s, v, g, norm, Cg, k, (bf16raw*)w2,
+                       (bf16raw*)w3);
+  else
+    hipLaunchKernelGGL(wn_apply_fwd_kernel<float>, dim3(C, 2), dim3(256), lds, s, v, g, norm, Cg, k, (float*)w2,
+                       (float*)w3);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfk_posconv_wnorm_bwd(const float* v, const float* g, const float* norm, const float* dw2, int32_t C,
+                                     int32_t Cg, int32_t k, float* ws, float* dv, float* dg, hipStream_t s) {
+  if (!v || !g || !norm || !dw2 || !ws || !dv || !dg || C <= 0 || Cg <= 0 || k <= 0 || C % Cg) return DFK_EINVAL;
+  const size_t lds = sizeof(float) * (size_t)Cg * k;
+  if (lds > 64 * 1024) return DFK_EINVAL;
+  hipLaunchKernelGGL(wn_partial_kernel, dim3(C), dim3(256), lds, s, v, dw2, Cg, k, ws);
+  hipLaunchKernelGGL(wn_reduce_kernel, dim3(k), dim3(256), 0, s, ws, C, k, const_cast<float*>(norm), dg);
+  hipLaunchKernelGGL(wn_apply_bwd_kernel, dim3(C), dim3(256), lds, s, v, g, norm, ws, dw2, Cg, k, dv);
+  DFK_CHECK_LAUNCH();
+  return 0;
+}

@@ -580,6 +580,39 @@ class ConvGeluFn(torch.autograd.Function):
         return dx, dw, None
 
 
+def _posconv_gemm_fwd(x, w2, bias, groups, k):
+    """y = x + gelu(conv(x) + b) as the implicit GEMM per (clip, group); returns (y, pre-activation)."""
+    B, T, C = x.shape
+    Cg = C // groups
+    dt = x.dtype
+    y = torch.empty_like(x)
+    pre = torch.empty_like(x)
+    K.gemm(x, C, False, w2, k * Cg, False, T, Cg, k * Cg, y, C, dtype=K.L.dt(x), bias=compute_weight(bias, dt),
+           bias_bs1=Cg, act=1, aux=pre, ldaux=C, residual=x, ldr=C, nz=(B, groups), a_bs=(T * C, Cg),
+           b_bs=(0, Cg * k * Cg), c_bs=(T * C, Cg), r_bs=(T * C, Cg), a_conv=(Cg, 1, k // 2, T))
+    return y, pre
+
+
+def _posconv_gemm_bwd(x, dy, pre, w3, bias, groups, k):
+    """-> (dx, dw2 [C, k*Cg] fp32 in the forward operand's layout, bias's gradient for autograd (None when the
+    ParamStore already holds it))."""
+    B, T, C = x.shape
+    Cg = C // groups
+    dt = K.L.dt(x)
+    dy = dy.contiguous()
+    dpre = K.gelu_bwd(dy, pre)
+    db = grad_done(bias, K.colsum(dpre.view(-1, C), grad_sink(bias)))
+    dw2 = torch.zeros(C, k * Cg, device=x.device)
+    K.gemm(dpre, C, True, x, C, True, Cg, k * Cg, T, dw2, k * Cg, dtype=dt, c_f32=True, atomic=True,
+           splitk=2, nz=(B, groups), a_bs=(T * C, Cg), b_bs=(T * C, Cg), c_bs=(0, Cg * k * Cg),
+           b_conv=(Cg, 1, k // 2, T))
+    # dx = dy + transposed conv: kernel flipped, pad k/2-1  (W3[g*Cg+ci][u*Cg+co] = W[g*Cg+co][ci][k-1-u])
+    dx = dy.clone()
+    K.gemm(dpre, C, False, w3, k * Cg, False, T, Cg, k * Cg, dx, C, dtype=dt, beta=1.0, nz=(B, groups),
+           a_bs=(T * C, Cg), b_bs=(0, Cg * k * Cg), c_bs=(T * C, Cg), a_conv=(Cg, 1, k // 2 - 1, T))
+    return dx, dw2, db
+
+
 class PosConvFn(torch.autograd.Function):
     """x + gelu(grouped Conv1d(C, C, k, pad k/2, groups G)(x) + b) with the last
     output frame dropped (HF modeling_wav2vec2.py:326-380,689-690); weight is
@@ -587,17 +620,11 @@ class PosConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, groups):
-        B, T, C = x.shape
+        C = x.shape[2]
         Cg = C // groups
         k = weight.shape[2]
-        pad = k // 2
-        dt = x.dtype
-        w2 = weight.detach().permute(0, 2, 1).reshape(C, k * Cg).to(dt).contiguous()  # [co][kk*Cg+ci]
-        y = torch.empty_like(x)
-        pre = torch.empty_like(x)
-        K.gemm(x, C, False, w2, k * Cg, False, T, Cg, k * Cg, y, C, dtype=K.L.dt(x), bias=compute_weight(bias, dt),
-               bias_bs1=Cg, act=1, aux=pre, ldaux=C, residual=x, ldr=C, nz=(B, groups), a_bs=(T * C, Cg),
-               b_bs=(0, Cg * k * Cg), c_bs=(T * C, Cg), r_bs=(T * C, Cg), a_conv=(Cg, 1, pad, T))
+        w2 = weight.detach().permute(0, 2, 1).reshape(C, k * Cg).to(x.dtype).contiguous()  # [co][kk*Cg+ci]
+        y, pre = _posconv_gemm_fwd(x, w2, bias, groups, k)
         grad_use(ctx, 2, bias)
         ctx.save_for_backward(x, weight, bias, pre)
         ctx.groups = groups
@@ -606,25 +633,50 @@ class PosConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight, bias, pre = ctx.saved_tensors
-        B, T, C = x.shape
-        G = ctx.groups
-        Cg = C // G
-        k = weight.shape[2]
-        dt = K.L.dt(x)
-        dy = dy.contiguous()
-        dpre = K.gelu_bwd(dy, pre)
-        db = grad_done(bias, K.colsum(dpre.view(-1, C), grad_sink(bias)))
-        dw2 = torch.zeros(C, k * Cg, device=x.device)
-        K.gemm(dpre, C, True, x, C, True, Cg, k * Cg, T, dw2, k * Cg, dtype=dt, c_f32=True, atomic=True,
-               splitk=2, nz=(B, G), a_bs=(T * C, Cg), b_bs=(T * C, Cg), c_bs=(0, Cg * k * Cg),
-               b_conv=(Cg, 1, k // 2, T))
-        # dx = dy + transposed conv: kernel flipped, pad k/2-1  (W3[g*Cg+ci][u*Cg+co] = W[g*Cg+co][ci][k-1-u])
+        C, G = x.shape[2], ctx.groups
+        Cg, k = C // G, weight.shape[2]
         w3 = weight.detach().view(G, Cg, Cg, k).flip(3).permute(0, 2, 3, 1).reshape(C, k * Cg).to(x.dtype).contiguous()
-        dx = dy.clone()
-        K.gemm(dpre, C, False, w3, k * Cg, False, T, Cg, k * Cg, dx, C, dtype=dt, beta=1.0, nz=(B, G),
-               a_bs=(T * C, Cg), b_bs=(0, Cg * k * Cg), c_bs=(T * C, Cg), a_conv=(Cg, 1, k // 2 - 1, T))
-        dw = dw2.view(C, k, Cg).permute(0, 2, 1)
-        return dx, dw, db, None
+        dx, dw2, db = _posconv_gemm_bwd(x, dy, pre, w3, bias, G, k)
+        return dx, dw2.view(C, k, Cg).permute(0, 2, 1), db, None
+
+
+class PosConvWNFn(torch.autograd.Function):
+    """PosConvFn with the weight norm inside (HF weight_norm(dim=2): w = g v / ||v||_(0,1),
+    modeling_wav2vec2.py:336-350): dfk_posconv_wnorm_fwd writes w straight into the forward GEMM's operand and the
+    input-gradient GEMM's flipped operand (no torch weight-norm ops, permutes or casts), dfk_posconv_wnorm_bwd turns
+    the dW GEMM's output into the gradients of g and v."""
+
+    @staticmethod
+    def forward(ctx, x, g, v, bias, groups):
+        C = x.shape[2]
+        Cg = C // groups
+        k = v.shape[2]
+        if v.shape[0] != C or v.shape[1] != Cg or g.numel() != k:
+            raise ValueError("PosConvWNFn: v must be [C, C/groups, k] and g [1, 1, k]")
+        vv, gg = v.detach().float().contiguous(), g.detach().float().contiguous()
+        norm = torch.empty(k, device=x.device)
+        ws = torch.empty(C * k, device=x.device)
+        w2 = torch.empty(C, k * Cg, device=x.device, dtype=x.dtype)
+        w3 = torch.empty_like(w2)
+        K.posconv_wnorm_fwd(vv, gg, C, Cg, k, norm, ws, w2, w3)
+        y, pre = _posconv_gemm_fwd(x, w2, bias, groups, k)
+        grad_use(ctx, 1, g)
+        grad_use(ctx, 2, v)
+        grad_use(ctx, 3, bias)
+        ctx.save_for_backward(x, gg, vv, bias, pre, w3, norm, g, v)
+        ctx.groups = groups
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gg, vv, bias, pre, w3, norm, g, v = ctx.saved_tensors
+        C, G = x.shape[2], ctx.groups
+        Cg, k = C // G, vv.shape[2]
+        dx, dw2, db = _posconv_gemm_bwd(x, dy, pre, w3, bias, G, k)
+        dv, dg = grad_sink(v), grad_sink(g)
+        ws = torch.empty(C * k, device=x.device)
+        K.posconv_wnorm_bwd(vv, gg, norm, dw2, C, Cg, k, ws, dv, dg)
+        return dx, grad_done(g, dg), grad_done(v, dv), db, None
 
 
 class CosineQKFn(torch.autograd.Function):

@@ -480,6 +480,18 @@ def gelu_bwd(dy, pre, out=None):
     return out
 
 
+def posconv_wnorm_fwd(v, g, C, Cg, k, norm, ws, w2, w3):
+    """norm[k] = ||v[:, :, k]||; w = g v / norm into the positional conv's two GEMM operand layouts (dfk.h)."""
+    L.check(L.lib().dfk_posconv_wnorm_fwd(L.ptr(v), L.ptr(g), C, Cg, k, L.ptr(norm), L.ptr(ws), L.ptr(w2), L.ptr(w3),
+                                          L.dt(w2), L.stream()), "posconv_wnorm_fwd")
+
+
+def posconv_wnorm_bwd(v, g, norm, dw2, C, Cg, k, ws, dv, dg):
+    """dv / dg (fp32, +=) of w = g v / ||v|| from dw2 [C, k*Cg] (the dW GEMM's output in w2's layout)."""
+    L.check(L.lib().dfk_posconv_wnorm_bwd(L.ptr(v), L.ptr(g), L.ptr(norm), L.ptr(dw2), C, Cg, k, L.ptr(ws), L.ptr(dv),
+                                          L.ptr(dg), L.stream()), "posconv_wnorm_bwd")
+
+
 def cast(x, dtype):
     y = torch.empty(x.shape, device=x.device, dtype=dtype)
     L.check(L.lib().dfk_cast(L.ptr(x), L.dt(x), L.ptr(y), L.dt(y), x.numel(), L.stream()), "cast")

@@ -23,6 +23,7 @@ parameters (as torch's SGD skips grad=None).  config.deterministic() turns all
 of them off (the parity setting, Q12).
 """
 import json
+import os
 
 import torch
 import torch.nn as nn
@@ -144,8 +145,11 @@ class Wav2Vec2PositionalConvEmbedding(nn.Module):
         return v * (g / v.pow(2).sum(dim=(0, 1), keepdim=True).sqrt())
 
     def add_to(self, x):
-        """x + pos_conv(x) fused (HF/:689-690)."""
-        return Fn.PosConvFn.apply(x, self.weight(), self.conv.bias, self.groups)
+        """x + pos_conv(x) fused (HF/:689-690), the weight norm inside the op (Fn.PosConvWNFn)."""
+        if os.environ.get("DFK_POSCONV_WN", "1") == "0":   # A/B: torch weight-norm ops + PosConvFn
+            return Fn.PosConvFn.apply(x, self.weight(), self.conv.bias, self.groups)
+        p = self.conv.parametrizations.weight
+        return Fn.PosConvWNFn.apply(x, p.original0, p.original1, self.conv.bias, self.groups)
 
 
 class Wav2Vec2Attention(nn.Module):

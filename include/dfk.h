@@ -352,6 +352,18 @@ int dfk_cpb_bias_bwd_many(const int64_t* desc, int32_t n, int32_t max_L, const f
 /* dx = dy * gelu'(pre) (exact-erf GELU backward, torch nn.GELU / HF ACT2FN["gelu"]). */
 int dfk_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, int dtype, hipStream_t stream);
 
+/* wav2vec2 positional-conv weight norm, HF weight_norm(conv, dim=2) (transformers modeling_wav2vec2.py:336-350;
+ * replaces its g * v / ||v|| parametrization): v [C][Cg][k] fp32 (weight_v), g [k] fp32 (weight_g).
+ * fwd: norm[k] = ||v[:, :, k]||; w = g v / norm written as the two operands of the grouped conv's implicit GEMMs
+ * (dtype DFK_BF16 / DFK_F32): w2 [C][k*Cg], w2[o][kk*Cg+i] = w[o][i][kk] (forward), and w3 [C][k*Cg],
+ * w3[gr*Cg+ci][u*Cg+co] = w[gr*Cg+co][ci][k-1-u] (the transposed conv of the input gradient).
+ * bwd: from dw2 [C][k*Cg] fp32 (the weight-gradient GEMM's output in w2's layout), dg += (dw . v) / norm and
+ * dv += g / norm dw - g (dw . v) / norm^3 v.  ws: C*k floats; Cg*k*4 bytes <= 64 KB; fixed summation order. */
+int dfk_posconv_wnorm_fwd(const float* v, const float* g, int32_t C, int32_t Cg, int32_t k, float* norm, float* ws,
+                          void* w2, void* w3, int dtype, hipStream_t stream);
+int dfk_posconv_wnorm_bwd(const float* v, const float* g, const float* norm, const float* dw2, int32_t C, int32_t Cg,
+                          int32_t k, float* ws, float* dv, float* dg, hipStream_t stream);
+
 /* torch.optim.SGD(momentum, weight_decay) step over a flat fp32 parameter
  * buffer (src/trainer.py:80-84,295), optionally writing the bf16 compute
  * shadow of the updated parameters in the same pass; lr read from device

@@ -85,6 +85,31 @@ def test_pos_conv(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_pos_conv_weight_norm(dt):
+    """PosConvWNFn (the weight norm w = g v / ||v||_(0,1) inside dfk_posconv_wnorm_fwd / _bwd, HF weight_norm(dim=2))
+    against torch fp32 (weight-norm autograd + conv1d): the output and the gradients of x, g, v and the bias."""
+    g = torch.Generator().manual_seed(3)
+    T = 49
+    x = torch.randn(2, T, 768, generator=g).to(DEV).to(dt).requires_grad_(True)
+    v = (torch.randn(768, 48, 128, generator=g) / 80).to(DEV).requires_grad_(True)
+    gw = (1.0 + 0.3 * torch.randn(1, 1, 128, generator=g)).to(DEV).requires_grad_(True)
+    b = (0.1 * torch.randn(768, generator=g)).to(DEV).requires_grad_(True)
+    y = Fn.PosConvWNFn.apply(x, gw, v, b, 16)
+    xr = x.detach().float().requires_grad_(True)
+    vr, gr, br = (t.detach().clone().requires_grad_(True) for t in (v, gw, b))
+    w = vr * (gr / vr.pow(2).sum(dim=(0, 1), keepdim=True).sqrt())
+    ref = xr + F.gelu(F.conv1d(xr.transpose(1, 2), w, br, padding=64, groups=16)[:, :, :-1]).transpose(1, 2)
+    t = 1e-4 if dt == torch.float32 else 2e-2
+    assert rel(y, ref) < t
+    dy = torch.randn(y.shape, generator=g).to(DEV).to(dt)
+    y.backward(dy)
+    ref.backward(dy.float())
+    tb = 1e-3 if dt == torch.float32 else 3e-2
+    for name, a, r in (("dx", x.grad, xr.grad), ("dg", gw.grad, gr.grad), ("dv", v.grad, vr.grad), ("db", b.grad, br.grad)):
+        assert rel(a, r) < tb, (name, rel(a, r))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_w2v_2layer_golden(dt):
     c = GC.W2V_C1
     fx = load(c["name"])
