@@ -3534,7 +3534,9 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
             da[kk] = *reinterpret_cast<const bf16x8*>(dOs + off);
           }
         };
-        int qb = __builtin_amdgcn_readfirstlane((kb + wave) % nb);   // spread the waves' first query blocks
+        // spread the waves' first query blocks; the offset is the round-robin wave of the unit, not the wave that runs
+        // it, so the dK / dV summation order (and the result, bit for bit) does not depend on the unit plan
+        int qb = __builtin_amdgcn_readfirstlane((kb + u % kB4Waves) % nb);
         load_old(qb);
         load_bias(qb);
         load_rows(qb);
@@ -3656,7 +3658,7 @@ __global__ __launch_bounds__(512) void wattn_bwd4_kernel(const dfk_wattn_bwd_arg
 #pragma unroll
           for (int eh = 0; eh < 2; ++eh) ka[eh] = tr16x2(kbase + vlo[eh], kbase + vhi[eh]);
         };
-        int kb = __builtin_amdgcn_readfirstlane((qb + wave) % nb);
+        int kb = __builtin_amdgcn_readfirstlane((qb + u % kB4Waves) % nb);   // as pass A: independent of the plan
         load_bias(kb);
         load_kv(kb);
         for (int i = 0; i < nb; ++i, kb = kb + 1 == nb ? 0 : kb + 1) {
