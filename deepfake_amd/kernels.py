@@ -169,12 +169,19 @@ def linear_dx(dy, w, out=None, act=0, aux=None, beta=0.0, drop=None, residual=No
         out = torch.empty(M, K, device=dy.device, dtype=dy.dtype)
     if residual is not None:
         residual = residual.contiguous()
+    if (_DX_BLAS and act == 0 and beta == 0.0 and drop is None and residual is None and M <= _DX_BLAS_MAX_M
+            and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dy.is_contiguous() and out.is_contiguous()):
+        # a plain product with no epilogue on the small-M shapes: the vendor library (hipBLASLt) runs it faster
+        # than the LDS-DMA kernel there (profiles/gemm/r6z_gemm_vs_hipblaslt.txt); the fused forms stay on dfk_gemm
+        return torch.matmul(dy, w, out=out)
     gemm(dy, dy.stride(0), False, w, w.stride(0), True, M, K, N, out, out.stride(0), dtype=L.dt(dy), act=act,
          aux=aux, ldaux=aux.stride(0) if aux is not None else 0, beta=beta, drop=drop, residual=residual,
          ldr=residual.stride(0) if residual is not None else 0)
     return out
 
 
+_DX_BLAS = os.environ.get("DFK_DX_BLAS", "1") == "1"   # plain small-M dX products on hipBLASLt (DFK_DX_BLAS=0: dfk_gemm)
+_DX_BLAS_MAX_M = int(os.environ.get("DFK_DX_BLAS_MAX_M", "131072"))
 _DW_MIN_K = int(os.environ.get("DFK_DW_MINK", "512"))   # tokens per split of a weight-gradient GEMM (tuning)
 _DW_UNSPLIT64 = int(os.environ.get("DFK_DW_UNSPLIT64", "384"))   # 64x64 tiles from which dW runs unsplit (r5o: the
 # 256-tile SwinV2 stage-3 fc1 / fc2 dW 22 -> 19, 21 -> 19 us on split 128x128 tiles; w2v (432-576 tiles) flat)
